@@ -1,0 +1,167 @@
+/*
+ * qsp_nmpc.h — C ABI of the MI355X batched pusher–slider NMPC solver.
+ *
+ * Drop-in boundary for the reference's solver backend: the acados MATLAB object
+ * `ocp_solver = acados_ocp(ocp_model, ocp_opts)` created in
+ * acados_nmpc/NMPC_controller.m:302-305 and driven through `.set/.solve/.get`
+ * (NMPC_controller.m:154-157, 170, 334-348, 382-394, 403, 420; helper.m:253, 264-269).
+ * One handle replaces B independent acados solver objects: every per-lane array is
+ * batched along a leading dimension B.  MATLAB column-major per-lane arrays
+ * (4 x (N+1), 2 x N, 4 x N) are exactly the row-major (N+1) x 4 / N x 2 / N x 4 blocks
+ * used here, so they pass through unchanged.
+ *
+ * Conventions
+ *   ownership : the caller owns host buffers; the handle owns device memory.
+ *   errors    : every entry point returns QSP_OK (0) or a negative QSP_ERR_*;
+ *               qsp_last_error() gives the message (thread-local).  Numerical
+ *               failure is NOT an error: it is the per-lane status (as acados 'status').
+ *   threading : one handle per host thread; a handle owns one HIP stream on one device.
+ *   precision : FP64 throughout.
+ */
+#ifndef QSP_NMPC_H
+#define QSP_NMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QSP_NX 4          /* x = [x, y, theta, s]   (PusherSliderModel.m:519) */
+#define QSP_NU 2          /* u = [u_n, u_t]         (PusherSliderModel.m:520) */
+#define QSP_NY 6
+#define QSP_NY_E 4
+#define QSP_NH 3          /* h = [s; u_n; u_t]      (NMPC_controller.m:237) */
+#define QSP_MAX_CTRL 64   /* spline control points per shape */
+
+#define QSP_OK 0
+#define QSP_ERR_ARG (-1)
+#define QSP_ERR_HIP (-2)
+#define QSP_ERR_STATE (-3)
+#define QSP_ERR_IO (-4)
+
+/* per-lane solver status (acados meaning where one exists) */
+#define QSP_STATUS_SUCCESS 0
+#define QSP_STATUS_NAN 1
+#define QSP_STATUS_MAXITER 2
+
+#define QSP_NLP_SQP_RTI_FIXED 0   /* K full Gauss-Newton steps: the BASELINE metric */
+
+typedef struct qsp_solver qsp_solver;
+
+/* Solver options: NMPC_controller.m:270-300 (create_ocp_opts) + dims. */
+typedef struct {
+    int32_t N;                /* horizon, param_scheme_N (NMPC_controller.m:281)        */
+    int32_t batch;            /* number of lanes B                                      */
+    int32_t nlp_mode;         /* QSP_NLP_*                                              */
+    int32_t sqp_iters;        /* K (fixed-K mode)                                       */
+    int32_t qp_iters;         /* max interior-point iterations per QP                   */
+    int32_t stages_per_lane;  /* S in the kernel's lane layout (0 = auto)               */
+    int32_t device;           /* HIP device ordinal                                     */
+    int32_t cost_scale_Ts;    /* 1: stage cost scaled by Ts as acados does             */
+    double Ts;                /* sample time, T = N * Ts (NMPC_controller.m:89,221)     */
+    double mu0, t_min, frac, sigma_min, mu_stop;  /* interior-point parameters         */
+} qsp_options;
+
+/* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */
+typedef struct {
+    int32_t n_ctrl;                     /* control points, first point repeated last   */
+    int32_t pad_;
+    double ctrl[QSP_MAX_CTRL][2];       /* contour points [m]                            */
+    double knots[QSP_MAX_CTRL + 4];     /* clamped cubic knot vector S (n_ctrl + 4)      */
+    double b;                           /* contour length (bspline_shape.m:37)           */
+    double c_ellipse;                   /* tau_max / (mu_sg m g)  (PusherSliderModel.m:55) */
+    double mu_sp;                       /* pusher-slider friction                        */
+} qsp_shape;
+
+/* Device-resident I/O for qsp_solve_device (all pointers on the handle's device). */
+typedef struct {
+    const double* x0;        /* B x 4              'constr_x0'                 */
+    const double* yref;      /* B x N x 6          'cost_y_ref' stages 0..N-1   */
+    const double* yref_e;    /* B x 4              'cost_y_ref_e'               */
+    const double* X_in;      /* B x (N+1) x 4      'init_x'                     */
+    const double* U_in;      /* B x N x 2          'init_u'                     */
+    const int32_t* shape_id; /* B (NULL: shape 0)                              */
+    double* u0;              /* B x 2              get('u', 0)                  */
+    double* X_out;           /* B x (N+1) x 4      get('x')                     */
+    double* U_out;           /* B x N x 2          get('u')                     */
+    double* PI_out;          /* B x N x 4          get('pi')                    */
+    int32_t* status;         /* B                  get('status')                */
+    double* cost;            /* B                  get_cost()                   */
+    int32_t controller;      /* 1: NMPC_controller.solve semantics (s pre-wrap, cold/warm start,
+                                tangential clip, Euler warm-start rollout, shifted X/U/PI out)    */
+    int32_t pad_;
+    uint8_t* warm_valid;     /* B, controller mode: 0 = cold start (set to 1 on exit); NULL = always cold */
+} qsp_device_io;
+
+/* ---------------------------------------------------------------- lifecycle */
+void qsp_default_options(qsp_options* opts);          /* N=20, B=1, K=50, Ts=0.05 ... */
+int qsp_create(const qsp_options* opts, qsp_solver** out);   /* acados_ocp(model, opts), :304 */
+int qsp_destroy(qsp_solver* s);
+const char* qsp_last_error(void);
+int qsp_version(void);
+int qsp_get_layout(const qsp_solver* s, int32_t* stages_per_lane, int32_t* lanes_per_instance);
+
+/* ------------------------------------------------------------- model / OCP */
+/* PLY contour -> ordered control points, knots, c_ellipse (PusherSliderModel.m:84-132, :53-55). */
+int qsp_shape_from_ply(const char* ply_path, int32_t flip, double mu_sg, double mu_sp, double mass,
+                       double tau_max, qsp_shape* out);
+int qsp_set_shapes(qsp_solver* s, const qsp_shape* shapes, int32_t n_shapes);
+int qsp_set_shape_ids(qsp_solver* s, const int32_t* shape_id /* B */);
+/* 'cost_W' (stages 0..N-1, diag of blkdiag(W_x, W_u)) and 'cost_W' at stage N (W_x_e)
+ * (NMPC_controller.m:153-164).  Only diagonal weights are supported. */
+int qsp_set_cost_W(qsp_solver* s, const double W_diag[6], const double W_e_diag[4]);
+/* 'constr_lh' / 'constr_uh' for h = [s; u_n; u_t] (NMPC_controller.m:251-252). */
+int qsp_set_constr_h(qsp_solver* s, const double lh[3], const double uh[3]);
+/* warm-start clip (update_tangential_velocity_bounds, NMPC_controller.m:98-100, 319-327) */
+int qsp_set_ctrl_params(qsp_solver* s, double v_alpha, double d_v_bound, double t_angle0, double u_n_lb,
+                        double u_t_ub);
+
+/* ------------------------------------------------- acados-level set/solve/get */
+int qsp_set_x0(qsp_solver* s, const double* x0 /* B x 4 */);                          /* 'constr_x0' */
+int qsp_set_yref(qsp_solver* s, const double* yref /* B x N x 6 */, const double* yref_e /* B x 4 */);
+int qsp_set_init(qsp_solver* s, const double* X /* B x (N+1) x 4 */, const double* U /* B x N x 2 */,
+                 const double* PI /* B x N x 4 or NULL */);                              /* 'init_*' */
+int qsp_solve(qsp_solver* s);                                                           /* .solve() */
+int qsp_get_u0(qsp_solver* s, double* u0 /* B x 2 */);                                  /* get('u',0) */
+int qsp_get_x(qsp_solver* s, double* X);
+int qsp_get_u(qsp_solver* s, double* U);
+int qsp_get_pi(qsp_solver* s, double* PI);
+int qsp_get_cost(qsp_solver* s, double* cost /* B */);
+int qsp_get_status(qsp_solver* s, int32_t* status /* B */);
+int qsp_get_sqp_iter(qsp_solver* s, int32_t* sqp_iter /* B */);
+int qsp_get_qp_iter(qsp_solver* s, int32_t* qp_iter /* B, summed over the SQP iterations */);
+int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
+
+/* --------------------------------------- NMPC_controller.solve(x0, index_time) */
+/* reference table y_ref (6 x T, MATLAB column-major == T x 6 row-major), shared by all lanes
+ * (set_reference_trajectory, NMPC_controller.m:425-431 with delay_buff_comp = 0) */
+int qsp_set_reference_trajectory(qsp_solver* s, const double* traj /* T x 6 */, int32_t T);
+/* x0: B x 4, index_time: B (1-based, as MATLAB).  Warm start lives on the device and is
+ * shifted after every call; u0 is available through qsp_get_u0. */
+int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_time);
+int qsp_controller_reset(qsp_solver* s);                                                 /* clear_variables */
+
+/* ------------------------------------------------ device-resident fast path */
+int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* hip_stream);
+int qsp_synchronize(qsp_solver* s);
+
+/* ------------------------------------------- building blocks (host arrays) */
+int qsp_eval_spline(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* sigma,
+                    double* C /* n x 2 */, double* D /* n x 2 */, double* Dd /* n x 2 */, double* kappa /* n */);
+int qsp_eval_dynamics(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* x, const double* u,
+                      double* f /* n x 4 */, double* J /* n x 4 x 6 */);
+int qsp_eval_rk4(qsp_solver* s, int32_t n, const int32_t* shape_id, double h, const double* x, const double* u,
+                 double* xn /* n x 4 */, double* A /* n x 4 x 4 */, double* B /* n x 4 x 2 */);
+int qsp_eval_vbound(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* sval, double* vb);
+/* Batched LQ-QP (interior point) with per-stage data; H and bound widths must be equal on
+ * every stage (as in the OCP).  H: nb x (6N+4) diag, g: nb x (6N+4), lo/hi: nb x N x 3,
+ * stage-0 s bound inactive. */
+int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, const double* b, const double* H,
+                 const double* g, const double* lo, const double* hi, const double* dx0, double* dx, double* du,
+                 double* pi, double* lam, int32_t* iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QSP_NMPC_H */

@@ -1,0 +1,185 @@
+"""ctypes binding of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Loads oracle/build/libqsp_oracle.so (built by oracle/Makefile).  Used by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg only.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from .shapes_np import shape_table
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libqsp_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+    return _lib
+
+
+class Opts(C.Structure):
+    _fields_ = [
+        ("N", C.c_int32), ("sqp_iters", C.c_int32), ("qp_iters", C.c_int32), ("stage0_s_bound", C.c_int32),
+        ("Ts", C.c_double), ("tau", C.c_double),
+        ("W", C.c_double * 6), ("We", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
+        ("mu0", C.c_double), ("t_min", C.c_double), ("frac", C.c_double),
+        ("sigma_min", C.c_double), ("mu_stop", C.c_double),
+        ("v_alpha", C.c_double), ("d_v", C.c_double), ("t_angle0", C.c_double),
+        ("u_n_lb", C.c_double), ("u_t_ub", C.c_double),
+        ("nlp_mode", C.c_int32), ("pad_", C.c_int32),
+        ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
+        ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
+    ]
+
+
+def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
+              W=(1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3), We=(2e5, 2e5, 20.0, 0.0),
+              lh=(-0.06, 0.0, -0.05), uh=(0.011, 0.03, 0.05),
+              mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
+              u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
+    o = Opts()
+    o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, 0
+    o.Ts = Ts
+    o.tau = Ts if tau is None else tau
+    o.W[:] = W
+    o.We[:] = We
+    o.lh[:] = lh
+    o.uh[:] = uh
+    o.mu0, o.t_min, o.frac = mu0, t_min, frac
+    o.sigma_min, o.mu_stop = sigma_min, mu_stop
+    o.v_alpha, o.d_v, o.t_angle0 = v_alpha, d_v, t_angle0
+    o.u_n_lb, o.u_t_ub = u_n_lb, u_t_ub
+    o.nlp_mode = nlp_mode
+    o.tol_stat = o.tol_eq = o.tol_ineq = o.tol_comp = tol
+    o.ls_alpha_min, o.ls_alpha_red, o.ls_eps = ls_alpha_min, ls_alpha_red, ls_eps
+    return o
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Oracle:
+    def __init__(self, names=("santal", "balea", "montana", "pulirapid"), max_ctrl=64):
+        self.tab = shape_table(names, max_ctrl)
+        t = self.tab
+        self._n = np.ascontiguousarray(t["n_ctrl"], np.int32)
+        self._c = np.ascontiguousarray(t["ctrl"], np.float64)
+        self._k = np.ascontiguousarray(t["knots"], np.float64)
+        self._pr = np.ascontiguousarray(t["params"], np.float64)
+        self._mc = int(max_ctrl)
+        self.L = lib()
+
+    def _shape_args(self):
+        return (_p(self._n), _p(self._c), _p(self._k), _p(self._pr), C.c_int(self._mc))
+
+    @staticmethod
+    def _ids(shape_id, n):
+        sid = np.zeros(n, np.int32) if shape_id is None else np.asarray(shape_id, np.int32)
+        if sid.shape == ():
+            sid = np.full(n, int(sid), np.int32)
+        return np.ascontiguousarray(sid)
+
+    def spline(self, s, shape_id=None):
+        s = np.ascontiguousarray(s, np.float64).ravel()
+        n = len(s)
+        sid = self._ids(shape_id, n)
+        Cv, dC, D, dD = (np.zeros((n, 2)) for _ in range(4))
+        kap = np.zeros(n)
+        self.L.or_spline_eval(*self._shape_args(), C.c_int32(n), _p(sid), _p(s), _p(Cv), _p(dC), _p(D), _p(dD), _p(kap))
+        return Cv, dC, D, dD, kap
+
+    def dynamics(self, x, u, shape_id=None):
+        x = np.ascontiguousarray(x, np.float64).reshape(-1, 4)
+        u = np.ascontiguousarray(u, np.float64).reshape(-1, 2)
+        n = len(x)
+        sid = self._ids(shape_id, n)
+        f = np.zeros((n, 4))
+        J = np.zeros((n, 4, 6))
+        self.L.or_dynamics(*self._shape_args(), C.c_int32(n), _p(sid), _p(x), _p(u), _p(f), _p(J))
+        return f, J
+
+    def rk4(self, x, u, h=0.05, shape_id=None):
+        x = np.ascontiguousarray(x, np.float64).reshape(-1, 4)
+        u = np.ascontiguousarray(u, np.float64).reshape(-1, 2)
+        n = len(x)
+        sid = self._ids(shape_id, n)
+        xn = np.zeros((n, 4))
+        A = np.zeros((n, 4, 4))
+        B = np.zeros((n, 4, 2))
+        self.L.or_rk4(*self._shape_args(), C.c_int32(n), _p(sid), C.c_double(h), _p(x), _p(u), _p(xn), _p(A), _p(B))
+        return xn, A, B
+
+    def vbound(self, s, opts, shape_id=None):
+        s = np.ascontiguousarray(s, np.float64).ravel()
+        n = len(s)
+        sid = self._ids(shape_id, n)
+        vb = np.zeros(n)
+        self.L.or_vbound(*self._shape_args(), C.byref(opts), C.c_int32(n), _p(sid), _p(s), _p(vb))
+        return vb
+
+    def qp(self, opts, A, B, b, H, g, lo, hi, act, dx0):
+        N = opts.N
+        nb = A.shape[0]
+        arrs = [np.ascontiguousarray(a, np.float64) for a in (A, B, b, H, g, lo, hi)]
+        act = np.ascontiguousarray(act, np.uint8)
+        dx0 = np.ascontiguousarray(dx0, np.float64)
+        dx = np.zeros((nb, N + 1, 4))
+        du = np.zeros((nb, N, 2))
+        pi = np.zeros((nb, N, 4))
+        lam = np.zeros((nb, N, 6))
+        r = self.L.or_qp_batch(C.byref(opts), C.c_int32(nb), *[_p(a) for a in arrs], _p(act), _p(dx0),
+                               _p(dx), _p(du), _p(pi), _p(lam))
+        return dict(dx=dx, du=du, pi=pi, lam=lam, fail=r)
+
+    def ocp_solve(self, opts, x0, yref, yref_e, X=None, U=None, PI=None, shape_id=None, nthreads=0):
+        N = opts.N
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
+        nb = len(x0)
+        sid = self._ids(shape_id, nb)
+        yref = np.ascontiguousarray(np.broadcast_to(yref, (nb, N, 6)), np.float64)
+        yref_e = np.ascontiguousarray(np.broadcast_to(yref_e, (nb, 4)), np.float64)
+        X = np.zeros((nb, N + 1, 4)) if X is None else np.array(X, np.float64, copy=True).reshape(nb, N + 1, 4)
+        U = np.zeros((nb, N, 2)) if U is None else np.array(U, np.float64, copy=True).reshape(nb, N, 2)
+        PI = np.zeros((nb, N, 4)) if PI is None else np.array(PI, np.float64, copy=True).reshape(nb, N, 4)
+        lam = np.zeros((nb, N, 6))
+        status = np.zeros(nb, np.int32)
+        iters = np.zeros(nb, np.int32)
+        cost = np.zeros(nb)
+        self.L.or_ocp_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
+                            _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(cost), C.c_int(nthreads))
+        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, cost=cost)
+
+    def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0):
+        """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place."""
+        N = opts.N
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
+        nb = len(x0)
+        sid = self._ids(shape_id, nb)
+        traj = np.ascontiguousarray(traj, np.float64).reshape(-1, 6)
+        idx = np.ascontiguousarray(np.broadcast_to(np.asarray(index_time, np.int32), (nb,)), np.int32)
+        u0 = np.zeros((nb, 2))
+        status = np.zeros(nb, np.int32)
+        iters = np.zeros(nb, np.int32)
+        cost = np.zeros(nb)
+        self.L.or_controller_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
+                                   C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]),
+                                   _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(cost), C.c_int(nthreads))
+        return dict(u0=u0, status=status, iters=iters, cost=cost)
+
+    @staticmethod
+    def new_warm(nb, N):
+        return dict(X=np.zeros((nb, N + 1, 4)), U=np.zeros((nb, N, 2)), PI=np.zeros((nb, N, 4)),
+                    valid=np.zeros(nb, np.uint8))

@@ -1,0 +1,42 @@
+"""Build recipe for the HIP extension (libqsp_nmpc.so, gfx950).
+
+hipcc compiles the kernels and the C-ABI into one shared library in-tree, so it
+travels to the GPU box with the repository snapshot.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libqsp_nmpc.so")
+SOURCES = ["qsp_solver.hip", "qsp_capi.hip"]
+HEADERS = ["qsp_math.hpp", "qsp_types.h", "qsp_kernels.h", "../../include/qsp_nmpc.h"]
+ARCH = os.environ.get("QSP_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(PKG, "..", "include")]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    cmd += ["-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,698 @@
+// qsp_capi.hip — C ABI (include/qsp_nmpc.h): handle, device buffers, set/solve/get.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/qsp_nmpc.h"
+#include "qsp_kernels.h"
+
+using namespace qsp;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail(QSP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct qsp_solver {
+    qsp_options o;
+    SolveParams p;
+    int S = 1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int n_shapes = 0;
+    DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
+    DevBuf warm_valid, traj, index_time;
+    DevBuf scratch[12];
+    int32_t T = 0;
+    bool have_traj = false;
+    float last_ms = 0.0f;
+};
+
+// --------------------------------------------------------------- helpers
+static void fill_params(qsp_solver* s) {
+    SolveParams& p = s->p;
+    p.N = s->o.N;
+    p.nlp_mode = s->o.nlp_mode;
+    p.sqp_iters = s->o.sqp_iters;
+    p.qp_iters = s->o.qp_iters;
+    p.Ts = s->o.Ts;
+    p.tau = s->o.cost_scale_Ts ? s->o.Ts : 1.0;
+    p.mu0 = s->o.mu0;
+    p.t_min = s->o.t_min;
+    p.frac = s->o.frac;
+    p.sigma_min = s->o.sigma_min;
+    p.mu_stop = s->o.mu_stop;
+}
+
+static int auto_S(int N) {
+    // Register-resident layout: S = 1 keeps the per-lane state within 256 VGPRs.
+    (void)N;
+    return 1;
+}
+
+// Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
+static int read_ply_xy(const char* path, std::vector<float>& xy) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(QSP_ERR_IO, std::string("cannot open ") + path);
+    std::string hdr;
+    char line[512];
+    int nv = -1, nprop = 0;
+    bool binle = false;
+    while (std::fgets(line, sizeof line, f)) {
+        std::string l(line);
+        if (l.rfind("format binary_little_endian", 0) == 0) binle = true;
+        if (l.rfind("element vertex", 0) == 0) nv = std::atoi(l.c_str() + 14);
+        if (l.rfind("property float", 0) == 0) ++nprop;
+        if (l.rfind("property list", 0) == 0 && nv < 0) { std::fclose(f); return fail(QSP_ERR_IO, "unsupported PLY"); }
+        if (l.rfind("end_header", 0) == 0) break;
+    }
+    if (!binle || nv <= 0 || nprop < 2) { std::fclose(f); return fail(QSP_ERR_IO, std::string("unsupported PLY ") + path); }
+    std::vector<float> v((size_t)nv * nprop);
+    if (std::fread(v.data(), sizeof(float), v.size(), f) != v.size()) { std::fclose(f); return fail(QSP_ERR_IO, "short PLY"); }
+    std::fclose(f);
+    xy.resize((size_t)nv * 2);
+    for (int i = 0; i < nv; ++i) { xy[2 * i] = v[(size_t)i * nprop]; xy[2 * i + 1] = v[(size_t)i * nprop + 1]; }
+    return QSP_OK;
+}
+
+static int h2d(qsp_solver* s, DevBuf& b, const void* src, size_t bytes) {
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+static int d2h(qsp_solver* s, void* dst, const DevBuf& b, size_t bytes) {
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipMemcpyAsync(dst, b.p, bytes, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+static SolveArgs make_args(qsp_solver* s) {
+    SolveArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.p = s->p;
+    a.B = s->o.batch;
+    a.shapes = s->shapes.as<ShapeDev>();
+    a.shape_id = s->shape_id.as<int32_t>();
+    a.x0 = s->x0.as<double>();
+    a.yref = s->yref.as<double>();
+    a.yref_e = s->yref_e.as<double>();
+    a.X_in = s->X.as<double>();
+    a.U_in = s->U.as<double>();
+    a.u0 = s->u0.as<double>();
+    a.X_out = s->Xo.as<double>();
+    a.U_out = s->Uo.as<double>();
+    a.PI_out = s->PIo.as<double>();
+    a.status = s->status.as<int32_t>();
+    a.sqp_iter = s->sqp_iter.as<int32_t>();
+    a.qp_iter = s->qp_iter.as<int32_t>();
+    a.cost = s->cost.as<double>();
+    return a;
+}
+
+static int run_timed(qsp_solver* s, const SolveArgs& a) {
+    HIPCHK(hipEventRecord(s->ev0, s->stream));
+    HIPCHK(launch_sqp(a, s->S, s->stream));
+    HIPCHK(hipEventRecord(s->ev1, s->stream));
+    HIPCHK(hipEventSynchronize(s->ev1));
+    HIPCHK(hipEventElapsedTime(&s->last_ms, s->ev0, s->ev1));
+    return QSP_OK;
+}
+
+template <class T>
+static int stage_in(qsp_solver* s, DevBuf& b, const T* src, size_t count) {
+    HIPCHK(b.ensure(count * sizeof(T)));
+    HIPCHK(hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, s->stream));
+    return QSP_OK;
+}
+template <class T>
+static int stage_out(qsp_solver* s, T* dst, DevBuf& b, size_t count) {
+    HIPCHK(hipMemcpyAsync(dst, b.p, count * sizeof(T), hipMemcpyDeviceToHost, s->stream));
+    return QSP_OK;
+}
+
+static int check_ids(qsp_solver* s, int32_t n, const int32_t* ids) {
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "no shapes set");
+    for (int i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= s->n_shapes) return fail(QSP_ERR_ARG, "shape id out of range");
+    return QSP_OK;
+}
+
+__global__ void stage_yref_kernel(const double* traj, int T, const int32_t* index_time, int B, int N, double* yref,
+                                  double* yref_e) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    // get_y_ref (NMPC_controller.m:307-313): column index_time+k (1-based), clamped to the last
+    for (int k = 0; k < N; ++k) {
+        int idx = index_time[i] + k;
+        if (idx > T) idx = T;
+        if (idx < 1) idx = 1;
+        for (int c = 0; c < 6; ++c) yref[((size_t)i * N + k) * 6 + c] = traj[(size_t)(idx - 1) * 6 + c];
+    }
+    // terminal reference = last stage reference (:348)
+    for (int c = 0; c < 4; ++c) yref_e[(size_t)i * 4 + c] = yref[((size_t)i * N + N - 1) * 6 + c];
+}
+
+extern "C" {
+
+void qsp_default_options(qsp_options* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->N = 20;
+    o->batch = 1;
+    o->nlp_mode = QSP_NLP_SQP_RTI_FIXED;
+    o->sqp_iters = 50;
+    o->qp_iters = 20;
+    o->stages_per_lane = 0;
+    o->device = 0;
+    o->cost_scale_Ts = 1;
+    o->Ts = 0.05;
+    o->mu0 = 1.0;
+    o->t_min = 1e-2;
+    o->frac = 0.995;
+    o->sigma_min = 1e-2;
+    o->mu_stop = 1e-10;
+}
+
+int qsp_version(void) { return 1; }
+
+const char* qsp_last_error(void) { return g_err.c_str(); }
+
+int qsp_create(const qsp_options* o, qsp_solver** out) {
+    if (!o || !out) return fail(QSP_ERR_ARG, "qsp_create: null argument");
+    if (o->N < 1 || o->batch < 1) return fail(QSP_ERR_ARG, "qsp_create: N and batch must be >= 1");
+    if (o->nlp_mode != QSP_NLP_SQP_RTI_FIXED) return fail(QSP_ERR_ARG, "qsp_create: unsupported nlp_mode");
+    if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
+    if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");
+    int S = o->stages_per_lane > 0 ? o->stages_per_lane : auto_S(o->N);
+    if (S < 1 || S > 3) return fail(QSP_ERR_ARG, "qsp_create: stages_per_lane must be in 1..3");
+    if (lanes_per_instance(o->N, S) > 64)
+        return fail(QSP_ERR_ARG, "qsp_create: N+1 > 64*stages_per_lane (one instance must fit in a wavefront)");
+    HIPCHK(hipSetDevice(o->device));
+    qsp_solver* s = new qsp_solver();
+    s->o = *o;
+    s->S = S;
+    fill_params(s);
+    // reference defaults (main.m:82-90, NMPC_controller.m:16-26, 98-100, 251-252)
+    const double W[6] = {1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3};
+    const double We[4] = {2e5, 2e5, 20.0, 0.0};
+    const double lh[3] = {-0.06, 0.0, -0.05}, uh[3] = {0.011, 0.03, 0.05};
+    std::memcpy(s->p.W, W, sizeof W);
+    std::memcpy(s->p.We, We, sizeof We);
+    std::memcpy(s->p.lh, lh, sizeof lh);
+    std::memcpy(s->p.uh, uh, sizeof uh);
+    s->p.cp = CtrlParams{1.0, 0.0, 3.0, 0.0, 0.05};
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&s->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&s->ev1);
+    const size_t B = o->batch, N = o->N;
+    auto al = [&](DevBuf& b, size_t bytes) { if (e == hipSuccess) e = b.ensure(bytes); };
+    al(s->shape_id, B * 4);
+    al(s->x0, B * 4 * 8);
+    al(s->yref, B * N * 6 * 8);
+    al(s->yref_e, B * 4 * 8);
+    al(s->X, B * (N + 1) * 4 * 8);
+    al(s->U, B * N * 2 * 8);
+    al(s->PI, B * N * 4 * 8);
+    al(s->Xo, B * (N + 1) * 4 * 8);
+    al(s->Uo, B * N * 2 * 8);
+    al(s->PIo, B * N * 4 * 8);
+    al(s->u0, B * 2 * 8);
+    al(s->status, B * 4);
+    al(s->sqp_iter, B * 4);
+    al(s->qp_iter, B * 4);
+    al(s->cost, B * 8);
+    al(s->warm_valid, B);
+    if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->warm_valid.p, 0, B, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->X.p, 0, B * (N + 1) * 4 * 8, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->U.p, 0, B * N * 2 * 8, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->PI.p, 0, B * N * 4 * 8, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) {
+        std::string m = std::string("qsp_create: ") + hipGetErrorString(e);
+        qsp_destroy(s);
+        return fail(QSP_ERR_HIP, m);
+    }
+    *out = s;
+    return QSP_OK;
+}
+
+int qsp_destroy(qsp_solver* s) {
+    if (!s) return QSP_OK;
+    (void)hipSetDevice(s->o.device);
+    DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
+                      &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
+                      &s->traj, &s->index_time};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& b : s->scratch) b.release();
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return QSP_OK;
+}
+
+int qsp_get_layout(const qsp_solver* s, int32_t* S, int32_t* L) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_get_layout: null handle");
+    if (S) *S = s->S;
+    if (L) *L = lanes_per_instance(s->o.N, s->S);
+    return QSP_OK;
+}
+
+// ------------------------------------------------------------------ shapes
+int qsp_shape_from_ply(const char* path, int32_t flip, double mu_sg, double mu_sp, double mass, double tau_max,
+                       qsp_shape* out) {
+    if (!path || !out) return fail(QSP_ERR_ARG, "qsp_shape_from_ply: null argument");
+    std::vector<float> P;
+    int r = read_ply_xy(path, P);
+    if (r != QSP_OK) return r;
+    const int n0 = (int)(P.size() / 2);
+    if (n0 + 1 > QSP_MAX_CTRL) return fail(QSP_ERR_ARG, "qsp_shape_from_ply: too many points");
+    // sortCadPoints (PusherSliderModel.m:84-111): start at the first min-x point, then
+    // greedy nearest neighbour in float32 with first-index ties; consumed points -> Inf.
+    std::vector<float> xs(P);
+    const float inf = INFINITY;
+    int ind = 0;
+    for (int i = 1; i < n0; ++i) if (xs[2 * i] < xs[2 * ind]) ind = i;
+    float tx = xs[2 * ind], ty = xs[2 * ind + 1];
+    xs[2 * ind] = xs[2 * ind + 1] = inf;
+    std::vector<double> srt((size_t)(n0 + 1) * 2);
+    srt[0] = tx; srt[1] = ty;
+    for (int i = 1; i < n0; ++i) {
+        int best = -1;
+        float bd = 0.0f;
+        for (int q = 0; q < n0; ++q) {
+            const float dx = xs[2 * q] - tx, dy = xs[2 * q + 1] - ty;
+            const float d = std::sqrt(dx * dx + dy * dy);
+            if (best < 0 || d < bd) { best = q; bd = d; }
+        }
+        tx = xs[2 * best]; ty = xs[2 * best + 1];
+        srt[2 * i] = tx; srt[2 * i + 1] = ty;
+        xs[2 * best] = xs[2 * best + 1] = inf;
+    }
+    const double sc = 1.0 / 1000.0;   // scale_factor (PusherSliderModel.m:72,105)
+    for (int i = 0; i < n0; ++i) { srt[2 * i] *= sc; srt[2 * i + 1] *= sc; }
+    srt[2 * n0] = srt[0]; srt[2 * n0 + 1] = srt[1];   // close the loop (:106)
+    const int n = n0 + 1;
+    if (flip) {   // flipud for montana / pulirapid (:107-109)
+        for (int i = 0; i < n / 2; ++i)
+            for (int c = 0; c < 2; ++c) std::swap(srt[2 * i + c], srt[2 * (n - 1 - i) + c]);
+    }
+    std::memset(out, 0, sizeof(*out));
+    out->n_ctrl = n;
+    for (int i = 0; i < n; ++i) { out->ctrl[i][0] = srt[2 * i]; out->ctrl[i][1] = srt[2 * i + 1]; }
+    // knots (getSpline :117-123): p = 3, m = n - 2, S = [0 0 0 linspace(0,b,m) b b b]
+    double b = 0.0;
+    for (int i = 0; i + 1 < n; ++i) {
+        const double dx = out->ctrl[i + 1][0] - out->ctrl[i][0], dy = out->ctrl[i + 1][1] - out->ctrl[i][1];
+        b += std::sqrt(dx * dx + dy * dy);
+    }
+    const int m = n - 2;
+    for (int i = 0; i < 3; ++i) out->knots[i] = 0.0;
+    const double step = b / (double)(m - 1);
+    for (int i = 0; i < m; ++i) out->knots[3 + i] = (i == m - 1) ? b : (double)i * step;
+    for (int i = 0; i < 3; ++i) out->knots[3 + m + i] = b;
+    out->b = b;
+    out->c_ellipse = tau_max / (mu_sg * mass * 9.81);   // :53,55 with helper.g = 9.81
+    out->mu_sp = mu_sp;
+    return QSP_OK;
+}
+
+int qsp_set_shapes(qsp_solver* s, const qsp_shape* shapes, int32_t n) {
+    if (!s || !shapes || n < 1) return fail(QSP_ERR_ARG, "qsp_set_shapes: bad argument");
+    std::vector<ShapeDev> h((size_t)n);
+    for (int q = 0; q < n; ++q) {
+        const qsp_shape& in = shapes[q];
+        ShapeDev& d = h[q];
+        std::memset(&d, 0, sizeof d);
+        const int nc = in.n_ctrl;
+        if (nc < 5 || nc > QSP_MAX_CTRL) return fail(QSP_ERR_ARG, "qsp_set_shapes: n_ctrl out of range");
+        d.n = nc;
+        d.b = in.b;
+        d.c = in.c_ellipse;
+        d.mu = in.mu_sp;
+        for (int i = 0; i < nc + 4; ++i) d.knots[i] = in.knots[i];
+        for (int i = 0; i < nc; ++i) { d.ctrl[2 * i] = in.ctrl[i][0]; d.ctrl[2 * i + 1] = in.ctrl[i][1]; }
+        const double h0 = in.knots[4] - in.knots[3];
+        d.inv_h = h0 > 0.0 ? 1.0 / h0 : 0.0;
+        // derivative-spline coefficients (bspline_shape.m:92-99 with zero-denominator guard :93)
+        for (int i = 1; i < nc; ++i) {
+            const double den = d.knots[i + 3] - d.knots[i];
+            for (int c = 0; c < 2; ++c)
+                d.dctrl[2 * i + c] = den != 0.0 ? 3.0 * ((d.ctrl[2 * i + c] - d.ctrl[2 * (i - 1) + c]) / den) : 0.0;
+        }
+        for (int i = 2; i < nc; ++i) {
+            const double den = d.knots[i + 2] - d.knots[i];
+            for (int c = 0; c < 2; ++c)
+                d.ddctrl[2 * i + c] = den != 0.0 ? 2.0 * ((d.dctrl[2 * i + c] - d.dctrl[2 * (i - 1) + c]) / den) : 0.0;
+        }
+    }
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(s->shapes.ensure(sizeof(ShapeDev) * n));
+    HIPCHK(hipMemcpyAsync(s->shapes.p, h.data(), sizeof(ShapeDev) * n, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->n_shapes = n;
+    return QSP_OK;
+}
+
+int qsp_set_shape_ids(qsp_solver* s, const int32_t* ids) {
+    if (!s || !ids) return fail(QSP_ERR_ARG, "qsp_set_shape_ids: null argument");
+    for (int i = 0; i < s->o.batch; ++i)
+        if (ids[i] < 0 || ids[i] >= s->n_shapes) return fail(QSP_ERR_ARG, "qsp_set_shape_ids: id out of range");
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipMemcpy(s->shape_id.p, ids, (size_t)s->o.batch * 4, hipMemcpyHostToDevice));
+    return QSP_OK;
+}
+
+int qsp_set_cost_W(qsp_solver* s, const double W[6], const double We[4]) {
+    if (!s || !W || !We) return fail(QSP_ERR_ARG, "qsp_set_cost_W: null argument");
+    for (int i = 0; i < 6; ++i) if (!(W[i] >= 0.0)) return fail(QSP_ERR_ARG, "qsp_set_cost_W: W must be >= 0");
+    for (int i = 0; i < 4; ++i) if (!(We[i] >= 0.0)) return fail(QSP_ERR_ARG, "qsp_set_cost_W: W_e must be >= 0");
+    if (!(W[4] > 0.0 && W[5] > 0.0)) return fail(QSP_ERR_ARG, "qsp_set_cost_W: control weights must be > 0");
+    std::memcpy(s->p.W, W, sizeof(double) * 6);
+    std::memcpy(s->p.We, We, sizeof(double) * 4);
+    return QSP_OK;
+}
+
+int qsp_set_constr_h(qsp_solver* s, const double lh[3], const double uh[3]) {
+    if (!s || !lh || !uh) return fail(QSP_ERR_ARG, "qsp_set_constr_h: null argument");
+    for (int i = 0; i < 3; ++i) if (!(lh[i] < uh[i])) return fail(QSP_ERR_ARG, "qsp_set_constr_h: need lh < uh");
+    std::memcpy(s->p.lh, lh, sizeof(double) * 3);
+    std::memcpy(s->p.uh, uh, sizeof(double) * 3);
+    return QSP_OK;
+}
+
+int qsp_set_ctrl_params(qsp_solver* s, double v_alpha, double d_v, double t_angle0, double u_n_lb, double u_t_ub) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_set_ctrl_params: null handle");
+    s->p.cp = CtrlParams{v_alpha, d_v, t_angle0, u_n_lb, u_t_ub};
+    return QSP_OK;
+}
+
+// --------------------------------------------------------- acados level
+int qsp_set_x0(qsp_solver* s, const double* x0) {
+    if (!s || !x0) return fail(QSP_ERR_ARG, "qsp_set_x0: null argument");
+    return h2d(s, s->x0, x0, (size_t)s->o.batch * 4 * 8);
+}
+
+int qsp_set_yref(qsp_solver* s, const double* yref, const double* yref_e) {
+    if (!s || !yref || !yref_e) return fail(QSP_ERR_ARG, "qsp_set_yref: null argument");
+    int r = h2d(s, s->yref, yref, (size_t)s->o.batch * s->o.N * 6 * 8);
+    if (r) return r;
+    return h2d(s, s->yref_e, yref_e, (size_t)s->o.batch * 4 * 8);
+}
+
+int qsp_set_init(qsp_solver* s, const double* X, const double* U, const double* PI) {
+    if (!s || !X || !U) return fail(QSP_ERR_ARG, "qsp_set_init: null argument");
+    const size_t B = s->o.batch, N = s->o.N;
+    int r = h2d(s, s->X, X, B * (N + 1) * 4 * 8);
+    if (!r) r = h2d(s, s->U, U, B * N * 2 * 8);
+    if (!r && PI) r = h2d(s, s->PI, PI, B * N * 4 * 8);
+    return r;
+}
+
+int qsp_solve(qsp_solver* s) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_solve: null handle");
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_solve: no shapes set");
+    HIPCHK(hipSetDevice(s->o.device));
+    SolveArgs a = make_args(s);
+    return run_timed(s, a);
+}
+
+int qsp_get_u0(qsp_solver* s, double* u0) {
+    if (!s || !u0) return fail(QSP_ERR_ARG, "qsp_get_u0: null argument");
+    return d2h(s, u0, s->u0, (size_t)s->o.batch * 2 * 8);
+}
+int qsp_get_x(qsp_solver* s, double* X) {
+    if (!s || !X) return fail(QSP_ERR_ARG, "qsp_get_x: null argument");
+    return d2h(s, X, s->Xo, (size_t)s->o.batch * (s->o.N + 1) * 4 * 8);
+}
+int qsp_get_u(qsp_solver* s, double* U) {
+    if (!s || !U) return fail(QSP_ERR_ARG, "qsp_get_u: null argument");
+    return d2h(s, U, s->Uo, (size_t)s->o.batch * s->o.N * 2 * 8);
+}
+int qsp_get_pi(qsp_solver* s, double* PI) {
+    if (!s || !PI) return fail(QSP_ERR_ARG, "qsp_get_pi: null argument");
+    return d2h(s, PI, s->PIo, (size_t)s->o.batch * s->o.N * 4 * 8);
+}
+int qsp_get_cost(qsp_solver* s, double* c) {
+    if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_cost: null argument");
+    return d2h(s, c, s->cost, (size_t)s->o.batch * 8);
+}
+int qsp_get_status(qsp_solver* s, int32_t* st) {
+    if (!s || !st) return fail(QSP_ERR_ARG, "qsp_get_status: null argument");
+    return d2h(s, st, s->status, (size_t)s->o.batch * 4);
+}
+int qsp_get_sqp_iter(qsp_solver* s, int32_t* it) {
+    if (!s || !it) return fail(QSP_ERR_ARG, "qsp_get_sqp_iter: null argument");
+    return d2h(s, it, s->sqp_iter, (size_t)s->o.batch * 4);
+}
+int qsp_get_qp_iter(qsp_solver* s, int32_t* it) {
+    if (!s || !it) return fail(QSP_ERR_ARG, "qsp_get_qp_iter: null argument");
+    return d2h(s, it, s->qp_iter, (size_t)s->o.batch * 4);
+}
+int qsp_get_time_tot(qsp_solver* s, double* ms) {
+    if (!s || !ms) return fail(QSP_ERR_ARG, "qsp_get_time_tot: null argument");
+    *ms = (double)s->last_ms;
+    return QSP_OK;
+}
+
+// ------------------------------------------------------ controller level
+int qsp_set_reference_trajectory(qsp_solver* s, const double* traj, int32_t T) {
+    if (!s || !traj || T < 1) return fail(QSP_ERR_ARG, "qsp_set_reference_trajectory: bad argument");
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(s->traj.ensure((size_t)T * 6 * 8));
+    HIPCHK(hipMemcpyAsync(s->traj.p, traj, (size_t)T * 6 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->T = T;
+    s->have_traj = true;
+    return QSP_OK;
+}
+
+int qsp_controller_reset(qsp_solver* s) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_controller_reset: null handle");
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipMemsetAsync(s->warm_valid.p, 0, (size_t)s->o.batch, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_time) {
+    if (!s || !x0 || !index_time) return fail(QSP_ERR_ARG, "qsp_controller_solve: null argument");
+    if (!s->have_traj) return fail(QSP_ERR_STATE, "qsp_controller_solve: no reference trajectory");
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_controller_solve: no shapes set");
+    const size_t B = s->o.batch;
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(s->index_time.ensure(B * 4));
+    HIPCHK(hipMemcpyAsync(s->x0.p, x0, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->index_time.p, index_time, B * 4, hipMemcpyHostToDevice, s->stream));
+    hipLaunchKernelGGL(stage_yref_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s->stream,
+                       s->traj.as<double>(), s->T, s->index_time.as<int32_t>(), (int)B, s->o.N, s->yref.as<double>(),
+                       s->yref_e.as<double>());
+    HIPCHK(hipGetLastError());
+    SolveArgs a = make_args(s);
+    a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
+    a.warm_valid = s->warm_valid.as<uint8_t>();
+    // warm buffers are updated in place (each instance reads its own stages before writing)
+    a.X_out = s->X.as<double>();
+    a.U_out = s->U.as<double>();
+    a.PI_out = s->PI.as<double>();
+    return run_timed(s, a);
+}
+
+// ------------------------------------------------------ device fast path
+int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
+    if (!s || !io) return fail(QSP_ERR_ARG, "qsp_solve_device: null argument");
+    if (!io->x0 || !io->yref || !io->yref_e || !io->X_in || !io->U_in || !io->u0 || !io->X_out || !io->U_out ||
+        !io->PI_out || !io->status || !io->cost)
+        return fail(QSP_ERR_ARG, "qsp_solve_device: missing device pointer");
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_solve_device: no shapes set");
+    HIPCHK(hipSetDevice(s->o.device));
+    SolveArgs a = make_args(s);
+    a.x0 = io->x0;
+    a.yref = io->yref;
+    a.yref_e = io->yref_e;
+    a.X_in = io->X_in;
+    a.U_in = io->U_in;
+    a.shape_id = io->shape_id ? io->shape_id : s->shape_id.as<int32_t>();
+    a.u0 = io->u0;
+    a.X_out = io->X_out;
+    a.U_out = io->U_out;
+    a.PI_out = io->PI_out;
+    a.status = io->status;
+    a.cost = io->cost;
+    if (io->controller) {
+        a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
+        a.warm_valid = io->warm_valid;
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    HIPCHK(launch_sqp(a, s->S, st));
+    return QSP_OK;
+}
+
+int qsp_synchronize(qsp_solver* s) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_synchronize: null handle");
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+// ------------------------------------------------------- building blocks
+int qsp_eval_spline(qsp_solver* s, int32_t n, const int32_t* sid, const double* sig, double* C, double* D, double* Dd,
+                    double* kappa) {
+    if (!s || !sid || !sig || !C || !D || !Dd || !kappa || n < 1) return fail(QSP_ERR_ARG, "qsp_eval_spline: bad argument");
+    int r = check_ids(s, n, sid);
+    if (r) return r;
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    if ((r = stage_in(s, sc[0], sid, n)) || (r = stage_in(s, sc[1], sig, n))) return r;
+    HIPCHK(sc[2].ensure((size_t)n * 16)); HIPCHK(sc[3].ensure((size_t)n * 16));
+    HIPCHK(sc[4].ensure((size_t)n * 16)); HIPCHK(sc[5].ensure((size_t)n * 8));
+    HIPCHK(launch_spline(s->shapes.as<ShapeDev>(), sc[0].as<int32_t>(), n, sc[1].as<double>(), sc[2].as<double>(),
+                         sc[3].as<double>(), sc[4].as<double>(), sc[5].as<double>(), s->stream));
+    if ((r = stage_out(s, C, sc[2], (size_t)2 * n)) || (r = stage_out(s, D, sc[3], (size_t)2 * n)) ||
+        (r = stage_out(s, Dd, sc[4], (size_t)2 * n)) || (r = stage_out(s, kappa, sc[5], (size_t)n)))
+        return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_eval_dynamics(qsp_solver* s, int32_t n, const int32_t* sid, const double* x, const double* u, double* f,
+                      double* J) {
+    if (!s || !sid || !x || !u || !f || !J || n < 1) return fail(QSP_ERR_ARG, "qsp_eval_dynamics: bad argument");
+    int r = check_ids(s, n, sid);
+    if (r) return r;
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    if ((r = stage_in(s, sc[0], sid, n)) || (r = stage_in(s, sc[1], x, (size_t)4 * n)) ||
+        (r = stage_in(s, sc[2], u, (size_t)2 * n)))
+        return r;
+    HIPCHK(sc[3].ensure((size_t)n * 32)); HIPCHK(sc[4].ensure((size_t)n * 24 * 8));
+    HIPCHK(launch_dynamics(s->shapes.as<ShapeDev>(), sc[0].as<int32_t>(), n, sc[1].as<double>(), sc[2].as<double>(),
+                           sc[3].as<double>(), sc[4].as<double>(), s->stream));
+    if ((r = stage_out(s, f, sc[3], (size_t)4 * n)) || (r = stage_out(s, J, sc[4], (size_t)24 * n))) return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_eval_rk4(qsp_solver* s, int32_t n, const int32_t* sid, double h, const double* x, const double* u, double* xn,
+                 double* A, double* B) {
+    if (!s || !sid || !x || !u || !xn || !A || !B || n < 1) return fail(QSP_ERR_ARG, "qsp_eval_rk4: bad argument");
+    int r = check_ids(s, n, sid);
+    if (r) return r;
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    if ((r = stage_in(s, sc[0], sid, n)) || (r = stage_in(s, sc[1], x, (size_t)4 * n)) ||
+        (r = stage_in(s, sc[2], u, (size_t)2 * n)))
+        return r;
+    HIPCHK(sc[3].ensure((size_t)n * 32)); HIPCHK(sc[4].ensure((size_t)n * 128)); HIPCHK(sc[5].ensure((size_t)n * 64));
+    HIPCHK(launch_rk4(s->shapes.as<ShapeDev>(), sc[0].as<int32_t>(), n, h, sc[1].as<double>(), sc[2].as<double>(),
+                      sc[3].as<double>(), sc[4].as<double>(), sc[5].as<double>(), s->stream));
+    if ((r = stage_out(s, xn, sc[3], (size_t)4 * n)) || (r = stage_out(s, A, sc[4], (size_t)16 * n)) ||
+        (r = stage_out(s, B, sc[5], (size_t)8 * n)))
+        return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_eval_vbound(qsp_solver* s, int32_t n, const int32_t* sid, const double* sv, double* vb) {
+    if (!s || !sid || !sv || !vb || n < 1) return fail(QSP_ERR_ARG, "qsp_eval_vbound: bad argument");
+    int r = check_ids(s, n, sid);
+    if (r) return r;
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    if ((r = stage_in(s, sc[0], sid, n)) || (r = stage_in(s, sc[1], sv, n))) return r;
+    HIPCHK(sc[2].ensure((size_t)n * 8));
+    HIPCHK(launch_vbound(s->shapes.as<ShapeDev>(), sc[0].as<int32_t>(), n, s->p.cp, sc[1].as<double>(),
+                         sc[2].as<double>(), s->stream));
+    if ((r = stage_out(s, vb, sc[2], (size_t)n))) return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, const double* b, const double* H,
+                 const double* g, const double* lo, const double* hi, const double* dx0, double* dx, double* du,
+                 double* pi, double* lam, int32_t* iters) {
+    if (!s || nb < 1 || !A || !B || !b || !H || !g || !lo || !hi || !dx0 || !dx || !du || !pi || !lam || !iters)
+        return fail(QSP_ERR_ARG, "qsp_qp_solve: bad argument");
+    const int N = s->o.N;
+    QPArgs q;
+    std::memset(&q, 0, sizeof q);
+    q.p = s->p;
+    q.p.tau = 1.0;
+    for (int i = 0; i < 6; ++i) q.p.W[i] = H[i];
+    for (int i = 0; i < 4; ++i) q.p.We[i] = H[6 * N + i];
+    for (int j = 0; j < 3; ++j) q.width[j] = hi[j] - lo[j];
+    for (int l = 0; l < nb; ++l) {
+        for (int k = 0; k < N; ++k) {
+            for (int i = 0; i < 6; ++i)
+                if (H[(size_t)l * (6 * N + 4) + 6 * k + i] != q.p.W[i])
+                    return fail(QSP_ERR_ARG, "qsp_qp_solve: stage Hessian must be equal on every stage");
+            for (int j = 0; j < 3; ++j) {
+                const double w = hi[((size_t)l * N + k) * 3 + j] - lo[((size_t)l * N + k) * 3 + j];
+                if (std::fabs(w - q.width[j]) > 1e-12 * (1.0 + std::fabs(w)))
+                    return fail(QSP_ERR_ARG, "qsp_qp_solve: bound widths must be equal on every stage");
+            }
+        }
+        for (int i = 0; i < 4; ++i)
+            if (H[(size_t)l * (6 * N + 4) + 6 * N + i] != q.p.We[i])
+                return fail(QSP_ERR_ARG, "qsp_qp_solve: terminal Hessian must be equal on every lane");
+    }
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    int r;
+    if ((r = stage_in(s, sc[0], A, (size_t)nb * N * 16)) || (r = stage_in(s, sc[1], B, (size_t)nb * N * 8)) ||
+        (r = stage_in(s, sc[2], b, (size_t)nb * N * 4)) || (r = stage_in(s, sc[3], g, (size_t)nb * (6 * N + 4))) ||
+        (r = stage_in(s, sc[4], lo, (size_t)nb * N * 3)) || (r = stage_in(s, sc[5], dx0, (size_t)nb * 4)))
+        return r;
+    HIPCHK(sc[6].ensure((size_t)nb * (N + 1) * 32)); HIPCHK(sc[7].ensure((size_t)nb * N * 16));
+    HIPCHK(sc[8].ensure((size_t)nb * N * 32)); HIPCHK(sc[9].ensure((size_t)nb * N * 48));
+    HIPCHK(sc[10].ensure((size_t)nb * 4));
+    q.nb = nb;
+    q.A = sc[0].as<double>(); q.B = sc[1].as<double>(); q.b = sc[2].as<double>(); q.g = sc[3].as<double>();
+    q.lo = sc[4].as<double>(); q.dx0 = sc[5].as<double>();
+    q.dx = sc[6].as<double>(); q.du = sc[7].as<double>(); q.pi = sc[8].as<double>(); q.lam = sc[9].as<double>();
+    q.iters = sc[10].as<int32_t>();
+    HIPCHK(launch_qp(q, s->S, s->stream));
+    if ((r = stage_out(s, dx, sc[6], (size_t)nb * (N + 1) * 4)) || (r = stage_out(s, du, sc[7], (size_t)nb * N * 2)) ||
+        (r = stage_out(s, pi, sc[8], (size_t)nb * N * 4)) || (r = stage_out(s, lam, sc[9], (size_t)nb * N * 6)) ||
+        (r = stage_out(s, iters, sc[10], (size_t)nb)))
+        return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+}  // extern "C"
