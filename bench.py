@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: batched pusher-slider NMPC solves/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the configuration the metric is quoted on):
+  N = 20, batch = 65 536 lanes per GPU, 4 slider shapes mixed per lane
+  (shape_id = lane mod 4: santal/balea/montana/pulirapid), K = 50 SQP-RTI
+  (full Gauss-Newton) iterations, every lane a cold-start NMPC_controller.solve
+  (acados_nmpc/NMPC_controller.m:329-423), x0 drawn from the config-2 law
+  (ranges of main.m:53-56), x_ref = the config-1 straight line from index 1.
+A step is one batched solve of all lanes; inputs are resident in HBM before the
+timed region, which brackets exactly --steps kernel launches.
+
+Multi-GPU (torchrun): one process per GPU, each rank solves its own shard of
+65 536 lanes (weak scaling, no data-path collective); the timing is the max over
+ranks.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "NMPC solves/sec at N=20, batch=65 536; max |u0−u0_ref|"
+SHAPES = ("santal", "balea", "montana", "pulirapid")
+
+# Algorithmic FP64 flops of the kernel's arithmetic (hand count of
+# uclv_qs_pushing_matlab_amd/csrc/qsp_math.hpp + qsp_solver.hip, FMA = 2,
+# div/sqrt/sin/cos/fmod = 1):
+FLOP_LIN_STAGE = 2267   # RK4 + forward sensitivities + defect/gradient + rollout/update, per stage per SQP iteration
+FLOP_IPM_STAGE = 874    # one Mehrotra iteration (factor + 2 solves + barrier/step), per stage
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP64 matrix) peak, datasheet (MI355X_MICROARCH.md)
+
+
+def config2_x0(nb, seed):
+    rng = np.random.default_rng(seed)
+    return np.stack([rng.uniform(-0.0065, 0.0260, nb), rng.uniform(-0.0197, 0.0124, nb),
+                     np.deg2rad(rng.uniform(-8.05, 9.30, nb)), rng.uniform(-0.0382, 0.0011, nb)], 1)
+
+
+def straight_traj(T_end=10.0, Ts=0.05, v=0.01):
+    t = np.arange(0.0, T_end + 1e-9, Ts)
+    traj = np.zeros((len(t), 6))
+    traj[:, 0] = v * t
+    return traj
+
+
+def make_inputs(B, N, seed):
+    x0 = config2_x0(B, seed)
+    traj = straight_traj()
+    yref = np.broadcast_to(traj[None, :N], (B, N, 6)).copy()
+    yref_e = yref[:, N - 1, :4].copy()
+    shape_id = (np.arange(B) % len(SHAPES)).astype(np.int32)
+    return x0, yref, yref_e, shape_id, traj
+
+
+def shard_range(total, world, rank):
+    """Contiguous, balanced shard of `total` units for `rank` (covers every unit once)."""
+    base, rem = divmod(total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def flops_per_solve(N, K, qp_iter_total):
+    return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
+
+
+def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads):
+    """Oracle (port) timed on a bounded sample of the same workload (cold-start controller solves)."""
+    from oracle.oracle import Oracle, make_opts
+    orc = Oracle(SHAPES)
+    op = make_opts(N=N, sqp_iters=K)
+
+    def run(sl, xx=None):
+        xx = x0[sl] if xx is None else xx
+        warm = orc.new_warm(len(xx), N)
+        return orc.controller_solve(op, xx, traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
+
+    probe = min(len(x0), max(2 * threads, 16))
+    t0 = time.perf_counter()
+    run(slice(0, probe))
+    per = (time.perf_counter() - t0) / probe
+    n = int(min(len(x0), max(probe, target_s / max(per, 1e-7))))
+    n = min(len(x0), max(threads, (n // threads) * threads))
+    t0 = time.perf_counter()
+    r = run(slice(0, n))
+    dt = time.perf_counter() - t0
+    return n, dt, r, run
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=65536, help="lanes per GPU")
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--sqp-iters", type=int, default=50)
+    ap.add_argument("--qp-iters", type=int, default=20)
+    ap.add_argument("--stages-per-lane", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=20250303 + 3)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local_rank)
+
+    from uclv_qs_pushing_matlab_amd._lib import DeviceIO
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+
+    B, N, K = args.batch, args.N, args.sqp_iters
+    # this rank's shard of the global lane set (weak scaling: B lanes per GPU)
+    lo, hi = shard_range(B * world, world, rank)
+    x0_all, yref_all, yref_e_all, sid_all, traj = make_inputs(B * world, N, args.seed)
+    x0, yref, yref_e, sid = x0_all[lo:hi], yref_all[lo:hi], yref_e_all[lo:hi], sid_all[lo:hi]
+    Bl = hi - lo
+
+    solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
+                       device=local_rank)
+    solver.set_shapes([make_shape(n) for n in SHAPES])
+    S_layout, L_layout = solver.layout()
+
+    t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+    d_x0, d_yref, d_yref_e = t(x0), t(yref), t(yref_e)
+    d_sid = t(sid, torch.int32)
+    d_Xin = torch.zeros((Bl, N + 1, 4), dtype=torch.float64, device=dev)
+    d_Uin = torch.zeros((Bl, N, 2), dtype=torch.float64, device=dev)
+    d_u0 = torch.empty((Bl, 2), dtype=torch.float64, device=dev)
+    d_X = torch.empty((Bl, N + 1, 4), dtype=torch.float64, device=dev)
+    d_U = torch.empty((Bl, N, 2), dtype=torch.float64, device=dev)
+    d_PI = torch.empty((Bl, N, 4), dtype=torch.float64, device=dev)
+    d_st = torch.empty((Bl,), dtype=torch.int32, device=dev)
+    d_cost = torch.empty((Bl,), dtype=torch.float64, device=dev)
+    io = DeviceIO()
+    for name, ten in (("x0", d_x0), ("yref", d_yref), ("yref_e", d_yref_e), ("X_in", d_Xin), ("U_in", d_Uin),
+                      ("shape_id", d_sid), ("u0", d_u0), ("X_out", d_X), ("U_out", d_U), ("PI_out", d_PI),
+                      ("status", d_st), ("cost", d_cost)):
+        setattr(io, name, ten.data_ptr())
+    io.controller = 1          # NMPC_controller.solve semantics, cold start every step
+    io.warm_valid = None
+    # a dedicated stream: the kernels and the timing events are on the same queue
+    stream = torch.cuda.Stream(dev)
+    sh = stream.cuda_stream
+
+    for _ in range(args.warmup):
+        solver.solve_device(io, sh)
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        solver.solve_device(io, sh)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # per-lane IPM iteration counts of the (identical) timed solves -> algorithmic flops
+    solver.synchronize()
+    qp_iter = solver.get("qp_iter")
+    status = d_st.cpu().numpy()
+    u0 = d_u0.cpu().numpy()
+    flops_launch = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())
+    if dist:
+        tt = torch.tensor([flops_launch, float(np.count_nonzero(status))], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        flops_all, nbad = float(tt[0]), int(tt[1])
+    else:
+        flops_all, nbad = flops_launch, int(np.count_nonzero(status))
+
+    total_solves = B * world * args.steps
+    value = total_solves / elapsed
+    avg_kern_s = float(np.mean(kern_ms)) * 1e-3
+    achieved = flops_launch / avg_kern_s / 1e12
+
+    result = {
+        "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "BASELINE configs[2]: batch=65536 per GPU, N=20, 4 shapes mixed per lane, "
+                               "K=50 SQP-RTI iterations, cold-start NMPC_controller.solve per lane",
+                   "global_batch": B * world, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
+                   "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout},
+                   "parallelism": f"dp{world} (independent lane shards, no collective in the solve)"},
+        "kernel_ms_avg": avg_kern_s * 1e3,
+        "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
+        "status_nonzero_lanes": nbad,
+        "roofline": {"bound": "mfma", "peak_kind": "FP64 vector (= FP64 matrix) peak; the kernel is FP64-VALU bound",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_launch": flops_launch, "flops_per_solve_mean": flops_launch / Bl},
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("batch") == Bl and pm.get("N") == N and pm.get("sqp_iters") == K:
+                result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        threads = max(1, min(threads, 16))
+        n, dt, r, run = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads)
+        result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
+                                  "sample": f"{n} lanes of the same workload (oracle/qsp_oracle.c, OpenMP, "
+                                            f"{dt:.1f} s)"}
+        # parity on the sampled lanes: GPU u0 vs oracle u0 (same cold-start controller solve)
+        u0_ref = r["u0"]
+        d = np.abs(u0[:n] - u0_ref).max(1)
+        m = min(n, 512)
+        rp = run(slice(0, m), x0[:m] * (1 + 1e-13))
+        stable = np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
+        result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
+                            "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
+                            "stable_lanes": int(stable.sum()), "stable_checked": int(m),
+                            "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
+                            "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
+                                    "< 1e-9 under a 1e-13 relative perturbation of x0 (non-chaotic lane)"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    solver.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -132,10 +132,13 @@ def test_ocp_solve_config2_parity(gpu, oracle):
     gpu.solve()
     u0 = gpu.get_u0()
     assert np.all(gpu.get("status") == 0)
-    # stability of the oracle itself under a 1e-13 relative perturbation of x0
-    ref_p = oracle.ocp_solve(op, x0 * (1 + 1e-13), yref, yref_e, X=X0 * (1 + 1e-13))
-    stable = (np.abs(ref_p["U"] - ref["U"]).max(axis=(1, 2)) < 1e-9) & \
-             (np.abs(ref_p["cost"] - ref["cost"]) <= 1e-9 * (1.0 + np.abs(ref["cost"])))
+    # well-conditioned lanes: the oracle itself is insensitive to rounding-level perturbations of x0
+    stable = np.ones(nb, bool)
+    for pert in (lambda v: v * (1 + 1e-13), lambda v: v * (1 - 1e-13), lambda v: v + 1e-15):
+        xp = pert(x0)
+        ref_p = oracle.ocp_solve(op, xp, yref, yref_e, X=np.repeat(xp[:, None], N + 1, 1))
+        stable &= (np.abs(ref_p["U"] - ref["U"]).max(axis=(1, 2)) < 1e-9) & \
+                  (np.abs(ref_p["cost"] - ref["cost"]) <= 1e-9 * (1.0 + np.abs(ref["cost"])))
     d = np.abs(u0 - ref["U"][:, 0]).max(1)
     assert stable.mean() > 0.6
     assert d[stable].max() < 1e-6, (d[stable].max(), np.sort(d[stable])[-5:])

@@ -55,6 +55,7 @@ struct qsp_solver {
     int n_shapes = 0;
     DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
     DevBuf warm_valid, traj, index_time;
+    DevBuf wX, wU, wx0, wlin;
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
@@ -78,9 +79,9 @@ static void fill_params(qsp_solver* s) {
 }
 
 static int auto_S(int N) {
-    // Register-resident layout: S = 1 keeps the per-lane state within 256 VGPRs.
+    // Register-resident layout; S = 2 measured fastest at N = 20 (profiles/ROUND1.md).
     (void)N;
-    return 1;
+    return 2;
 }
 
 // Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
@@ -141,6 +142,10 @@ static SolveArgs make_args(qsp_solver* s) {
     a.sqp_iter = s->sqp_iter.as<int32_t>();
     a.qp_iter = s->qp_iter.as<int32_t>();
     a.cost = s->cost.as<double>();
+    a.wX = s->wX.as<double>();
+    a.wU = s->wU.as<double>();
+    a.wx0 = s->wx0.as<double>();
+    a.wlin = s->wlin.as<double>();
     return a;
 }
 
@@ -218,7 +223,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
     if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");
     int S = o->stages_per_lane > 0 ? o->stages_per_lane : auto_S(o->N);
-    if (S < 1 || S > 3) return fail(QSP_ERR_ARG, "qsp_create: stages_per_lane must be in 1..3");
+    if (S < 1 || S > 2) return fail(QSP_ERR_ARG, "qsp_create: stages_per_lane must be 1 or 2");
     if (lanes_per_instance(o->N, S) > 64)
         return fail(QSP_ERR_ARG, "qsp_create: N+1 > 64*stages_per_lane (one instance must fit in a wavefront)");
     HIPCHK(hipSetDevice(o->device));
@@ -256,6 +261,10 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->qp_iter, B * 4);
     al(s->cost, B * 8);
     al(s->warm_valid, B);
+    al(s->wX, B * (N + 1) * 4 * 8);
+    al(s->wU, B * N * 2 * 8);
+    al(s->wx0, B * 4 * 8);
+    al(s->wlin, B * (N + 1) * 24 * 8);
     if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->warm_valid.p, 0, B, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->X.p, 0, B * (N + 1) * 4 * 8, s->stream);
@@ -276,7 +285,7 @@ int qsp_destroy(qsp_solver* s) {
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
-                      &s->traj, &s->index_time};
+                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -649,47 +658,74 @@ int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, co
     if (!s || nb < 1 || !A || !B || !b || !H || !g || !lo || !hi || !dx0 || !dx || !du || !pi || !lam || !iters)
         return fail(QSP_ERR_ARG, "qsp_qp_solve: bad argument");
     const int N = s->o.N;
-    QPArgs q;
-    std::memset(&q, 0, sizeof q);
-    q.p = s->p;
-    q.p.tau = 1.0;
-    for (int i = 0; i < 6; ++i) q.p.W[i] = H[i];
-    for (int i = 0; i < 4; ++i) q.p.We[i] = H[6 * N + i];
-    for (int j = 0; j < 3; ++j) q.width[j] = hi[j] - lo[j];
+    SolveParams p = s->p;
+    p.tau = 1.0;
+    for (int i = 0; i < 6; ++i) p.W[i] = H[i];
+    for (int i = 0; i < 4; ++i) p.We[i] = H[6 * N + i];
+    // bounds in step space lo = lh - v, hi = uh - v with lh = 0, uh = width, v = -lo
+    for (int j = 0; j < 3; ++j) { p.lh[j] = 0.0; p.uh[j] = hi[j] - lo[j]; }
     for (int l = 0; l < nb; ++l) {
         for (int k = 0; k < N; ++k) {
             for (int i = 0; i < 6; ++i)
-                if (H[(size_t)l * (6 * N + 4) + 6 * k + i] != q.p.W[i])
+                if (H[(size_t)l * (6 * N + 4) + 6 * k + i] != p.W[i])
                     return fail(QSP_ERR_ARG, "qsp_qp_solve: stage Hessian must be equal on every stage");
             for (int j = 0; j < 3; ++j) {
                 const double w = hi[((size_t)l * N + k) * 3 + j] - lo[((size_t)l * N + k) * 3 + j];
-                if (std::fabs(w - q.width[j]) > 1e-12 * (1.0 + std::fabs(w)))
+                if (std::fabs(w - p.uh[j]) > 1e-12 * (1.0 + std::fabs(w)))
                     return fail(QSP_ERR_ARG, "qsp_qp_solve: bound widths must be equal on every stage");
             }
+            const double* Ak = A + ((size_t)l * N + k) * 16;
+            const double st[10] = {Ak[0] - 1.0, Ak[1], Ak[4], Ak[5] - 1.0, Ak[8], Ak[9], Ak[10] - 1.0, Ak[12], Ak[13], Ak[14]};
+            for (double v : st)
+                if (v != 0.0) return fail(QSP_ERR_ARG, "qsp_qp_solve: A lacks the pusher-slider structure");
         }
         for (int i = 0; i < 4; ++i)
-            if (H[(size_t)l * (6 * N + 4) + 6 * N + i] != q.p.We[i])
+            if (H[(size_t)l * (6 * N + 4) + 6 * N + i] != p.We[i])
                 return fail(QSP_ERR_ARG, "qsp_qp_solve: terminal Hessian must be equal on every lane");
+    }
+    // pack the workspace on the host: stage data SoA, v = -lo through X/U, x0 - X_0 = dx0
+    const size_t tot = (size_t)nb * (N + 1);
+    std::vector<double> lin(tot * 24, 0.0), X(tot * 4, 0.0), U((size_t)nb * N * 2, 0.0), x0(dx0, dx0 + (size_t)nb * 4);
+    for (int l = 0; l < nb; ++l) {
+        for (int k = 0; k <= N; ++k) {
+            const size_t gi = (size_t)l * (N + 1) + k;
+            if (k < N) {
+                const double* Ak = A + ((size_t)l * N + k) * 16;
+                const double av[6] = {Ak[2], Ak[3], Ak[6], Ak[7], Ak[11], Ak[15]};
+                for (int q = 0; q < 6; ++q) lin[(0 + q) * tot + gi] = av[q];
+                for (int q = 0; q < 8; ++q) lin[(6 + q) * tot + gi] = B[((size_t)l * N + k) * 8 + q];
+                for (int q = 0; q < 4; ++q) lin[(14 + q) * tot + gi] = b[((size_t)l * N + k) * 4 + q];
+                for (int q = 0; q < 6; ++q) lin[(18 + q) * tot + gi] = g[(size_t)l * (6 * N + 4) + 6 * k + q];
+                X[gi * 4 + 3] = -lo[((size_t)l * N + k) * 3 + 0];
+                U[((size_t)l * N + k) * 2 + 0] = -lo[((size_t)l * N + k) * 3 + 1];
+                U[((size_t)l * N + k) * 2 + 1] = -lo[((size_t)l * N + k) * 3 + 2];
+            } else {
+                for (int q = 0; q < 4; ++q) lin[(18 + q) * tot + gi] = g[(size_t)l * (6 * N + 4) + 6 * N + q];
+            }
+        }
+        // dx0 = wx0 - X_0 with X_0 = (0, 0, 0, -lo_s(0))  ->  wx0 = dx0 + X_0
+        x0[(size_t)l * 4 + 3] += X[(size_t)l * (N + 1) * 4 + 3];
     }
     HIPCHK(hipSetDevice(s->o.device));
     auto& sc = s->scratch;
     int r;
-    if ((r = stage_in(s, sc[0], A, (size_t)nb * N * 16)) || (r = stage_in(s, sc[1], B, (size_t)nb * N * 8)) ||
-        (r = stage_in(s, sc[2], b, (size_t)nb * N * 4)) || (r = stage_in(s, sc[3], g, (size_t)nb * (6 * N + 4))) ||
-        (r = stage_in(s, sc[4], lo, (size_t)nb * N * 3)) || (r = stage_in(s, sc[5], dx0, (size_t)nb * 4)))
+    if ((r = stage_in(s, sc[0], lin.data(), lin.size())) || (r = stage_in(s, sc[1], X.data(), X.size())) ||
+        (r = stage_in(s, sc[2], U.data(), U.size())) || (r = stage_in(s, sc[3], x0.data(), x0.size())))
         return r;
-    HIPCHK(sc[6].ensure((size_t)nb * (N + 1) * 32)); HIPCHK(sc[7].ensure((size_t)nb * N * 16));
-    HIPCHK(sc[8].ensure((size_t)nb * N * 32)); HIPCHK(sc[9].ensure((size_t)nb * N * 48));
-    HIPCHK(sc[10].ensure((size_t)nb * 4));
-    q.nb = nb;
-    q.A = sc[0].as<double>(); q.B = sc[1].as<double>(); q.b = sc[2].as<double>(); q.g = sc[3].as<double>();
-    q.lo = sc[4].as<double>(); q.dx0 = sc[5].as<double>();
-    q.dx = sc[6].as<double>(); q.du = sc[7].as<double>(); q.pi = sc[8].as<double>(); q.lam = sc[9].as<double>();
-    q.iters = sc[10].as<int32_t>();
-    HIPCHK(launch_qp(q, s->S, s->stream));
-    if ((r = stage_out(s, dx, sc[6], (size_t)nb * (N + 1) * 4)) || (r = stage_out(s, du, sc[7], (size_t)nb * N * 2)) ||
-        (r = stage_out(s, pi, sc[8], (size_t)nb * N * 4)) || (r = stage_out(s, lam, sc[9], (size_t)nb * N * 6)) ||
-        (r = stage_out(s, iters, sc[10], (size_t)nb)))
+    HIPCHK(sc[4].ensure((size_t)nb * (N + 1) * 32)); HIPCHK(sc[5].ensure((size_t)nb * N * 16));
+    HIPCHK(sc[6].ensure((size_t)nb * N * 32)); HIPCHK(sc[7].ensure((size_t)nb * N * 48));
+    HIPCHK(sc[8].ensure((size_t)nb * 4));
+    SolveArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.p = p;
+    a.B = nb;
+    a.wlin = sc[0].as<double>(); a.wX = sc[1].as<double>(); a.wU = sc[2].as<double>(); a.wx0 = sc[3].as<double>();
+    a.qp_dx = sc[4].as<double>(); a.qp_du = sc[5].as<double>(); a.PI_out = sc[6].as<double>();
+    a.qp_lam = sc[7].as<double>(); a.qp_iter = sc[8].as<int32_t>();
+    HIPCHK(launch_qp(a, s->S, s->stream));
+    if ((r = stage_out(s, dx, sc[4], (size_t)nb * (N + 1) * 4)) || (r = stage_out(s, du, sc[5], (size_t)nb * N * 2)) ||
+        (r = stage_out(s, pi, sc[6], (size_t)nb * N * 4)) || (r = stage_out(s, lam, sc[7], (size_t)nb * N * 6)) ||
+        (r = stage_out(s, iters, sc[8], (size_t)nb)))
         return r;
     HIPCHK(hipStreamSynchronize(s->stream));
     return QSP_OK;

@@ -30,28 +30,22 @@ struct SolveArgs {
     int32_t* sqp_iter;         // B
     int32_t* qp_iter;          // B (sum of IPM iterations)
     double* cost;              // B
+    // workspace (device, owned by the handle)
+    double* wX;                // B x (N+1) x 4   SQP iterate
+    double* wU;                // B x N x 2
+    double* wx0;               // B x 4           x0 after the controller's s pre-wrap
+    double* wlin;              // 24 x B(N+1)     stage data (A, B, defect, gradient), SoA
+    // QP-level interface only (qsp_qp_solve): when qp_dx != nullptr the QP kernel
+    // reports the QP solution instead of updating the iterate
+    double* qp_dx;             // B x (N+1) x 4
+    double* qp_du;             // B x N x 2
+    double* qp_lam;            // B x N x 6
 };
 
-struct QPArgs {
-    SolveParams p;             // tau = 1, W = stage Hessian diag, We = terminal Hessian diag
-    int32_t nb;
-    double width[3];           // hi - lo per bounded component (equal on every stage)
-    const double* A;           // nb x N x 16 (pusher-slider structure)
-    const double* B;           // nb x N x 8
-    const double* b;           // nb x N x 4
-    const double* g;           // nb x (6N + 4)
-    const double* lo;          // nb x N x 3
-    const double* dx0;         // nb x 4
-    double* dx;                // nb x (N+1) x 4
-    double* du;                // nb x N x 2
-    double* pi;                // nb x N x 4
-    double* lam;               // nb x N x 6
-    int32_t* iters;            // nb
-};
 
 int lanes_per_instance(int N, int S);
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream);
-hipError_t launch_qp(const QPArgs& a, int S, hipStream_t stream);
+hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream);
 hipError_t launch_dynamics(const ShapeDev* shapes, const int32_t* sid, int n, const double* x, const double* u,

@@ -12,6 +12,7 @@
 
 #include "qsp_types.h"
 
+
 namespace qsp {
 
 // ---------------------------------------------------------------- B-spline
@@ -247,7 +248,7 @@ __device__ __forceinline__ void rk4(const ShapeDev& sh, double h, const double x
     double Sa[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0}};
     double K[4] = {0, 0, 0, 0};
     double SK[4][4] = {{0}};
-#pragma unroll
+#pragma unroll 1   // sequential RK stages keep the register footprint of the VDE small
     for (int st = 0; st < 4; ++st) {
         const double aa = h * ca[st];
         double xs[4];

@@ -21,6 +21,10 @@
 #include "qsp_math.hpp"
 #include "qsp_kernels.h"
 
+#ifndef QSP_MIN_WAVES
+#define QSP_MIN_WAVES 1
+#endif
+
 namespace qsp {
 
 // ------------------------------------------------------------- group helpers
@@ -42,22 +46,39 @@ __device__ __forceinline__ int sidx(int i, int j) {
 }
 
 // ------------------------------------------------------------- per-lane state
+// Registers hold what the horizon recursions read on every step (stage model,
+// gradient, Riccati factors); LDS holds what only the stage-parallel phases touch
+// (iterate, slacks/multipliers, barrier terms, QP solution pieces).
+constexpr int BLOCK = 256;                 // threads per workgroup (4 waves)
+enum LdsField : int {
+    F_T = 0,      // 6  slacks        s_lo s_hi un_lo un_hi ut_lo ut_hi
+    F_LM = 6,     // 6  multipliers
+    F_V = 12,     // 3  bounded components of the SQP iterate (s_k, u_n, u_t)
+    F_DU = 15,    // 2  damped QP control step
+    F_VA = 17,    // 3  affine-predictor bounded components (ds, dun, dut)
+    F_VN = 20,    // 3  corrector bounded components
+    F_DX = 23,    // 4  final QP state step
+    F_HG = 27,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
+    F_COUNT = 33
+};
+template <int S>
+constexpr int lds_bytes() { return F_COUNT * S * BLOCK * 8; }
+
 template <int S>
 struct Stage {
-    // SQP iterate and stage data of the current linearisation
-    double x[S][4], u[S][2];
     double g[S][6];          // cost gradient (stage: tau W (y - y_ref); terminal: We (x - y_ref_e))
     double a[S][6];          // free entries of A_k (qsp_math.hpp rk4)
     double B[S][8];
     double bb[S][4];         // defect phi(x_k,u_k) - x_{k+1}
-    // interior point
-    double t[S][6], lm[S][6];   // slacks / multipliers: s_lo s_hi un_lo un_hi ut_lo ut_hi
-    double hg[S][6];            // barrier Hessian (0..2) and gradient (3..5) additions
     double K[S][8], Ri[S][3], Pb[S][4], kk[S][2];
-    double du[S][2];            // damped QP control step
-    double vn[S][3];            // last QP solution of the bounded components (ds, dun, dut)
-    double va[S][3];            // affine-predictor solution of the bounded components
-    double dx[S][4];            // final QP state step
+    double* lds;             // this thread's column of the workgroup's LDS block
+    __device__ __forceinline__ double& f(int field, int ls, int i) const { return lds[((field + i) * S + ls) * BLOCK]; }
+    __device__ __forceinline__ double& t(int ls, int q) const { return f(F_T, ls, q); }
+    __device__ __forceinline__ double& lm(int ls, int q) const { return f(F_LM, ls, q); }
+    __device__ __forceinline__ double& v(int ls, int i) const { return f(F_V, ls, i); }
+    __device__ __forceinline__ double& du(int ls, int i) const { return f(F_DU, ls, i); }
+    __device__ __forceinline__ double& dxs(int ls, int i) const { return f(F_DX, ls, i); }
+    __device__ __forceinline__ double& hg(int ls, int i) const { return f(F_HG, ls, i); }
 };
 
 struct Ctx {
@@ -69,13 +90,28 @@ struct Ctx {
 template <int S>
 __device__ __forceinline__ int kof(const Ctx& c, int ls) { return c.lig * S + ls; }
 
-// bounded component value of the QP step in slot ls
+// bounds of the QP step of slot ls: lo = lh - v, hi = uh - v, v = (s, u_n, u_t)
 template <int S>
 __device__ __forceinline__ void bnd_lohi(const SolveParams& p, const Stage<S>& st, int ls, double lo[3], double hi[3]) {
-    const double v0 = st.x[ls][3], v1 = st.u[ls][0], v2 = st.u[ls][1];
+    const double v0 = st.v(ls, 0), v1 = st.v(ls, 1), v2 = st.v(ls, 2);
     lo[0] = p.lh[0] - v0; hi[0] = p.uh[0] - v0;
     lo[1] = p.lh[1] - v1; hi[1] = p.uh[1] - v1;
     lo[2] = p.lh[2] - v2; hi[2] = p.uh[2] - v2;
+}
+
+// chain hand-over along the wavefront without an LDS round trip (DPP wave shift)
+// (lanes without a source keep their own value, so the move can be done in place)
+__device__ __forceinline__ double wave_from_next(double v) {   // lane i <- lane i+1
+    const int l = __double2loint(v), h = __double2hiint(v);
+    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_from_prev(double v) {   // lane i <- lane i-1
+    const int l = __double2loint(v), h = __double2hiint(v);
+    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
 }
 
 // --------------------------------------------------------- Riccati primitives
@@ -128,12 +164,15 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     double R00 = Hu[0] + (B[0] * PB[0][0] + B[2] * PB[1][0] + B[4] * PB[2][0] + B[6] * PB[3][0]);
     double R01 = B[0] * PB[0][1] + B[2] * PB[1][1] + B[4] * PB[2][1] + B[6] * PB[3][1];
     double R11 = Hu[1] + (B[1] * PB[0][1] + B[3] * PB[1][1] + B[5] * PB[2][1] + B[7] * PB[3][1]);
+    // S~ = B'PA = (PB)'A with the structure of A
     double St[2][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            St[i][j] = B[i] * PA[0][j] + B[2 + i] * PA[1][j] + B[4 + i] * PA[2][j] + B[6 + i] * PA[3][j];
+    for (int i = 0; i < 2; ++i) {
+        St[i][0] = PB[0][i];
+        St[i][1] = PB[1][i];
+        St[i][2] = PB[0][i] * a[0] + PB[1][i] * a[2] + PB[2][i];
+        St[i][3] = PB[0][i] * a[1] + PB[1][i] * a[3] + PB[2][i] * a[4] + PB[3][i] * a[5];
+    }
     double rt[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) rt[i] = gu[i] + (B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3]);
@@ -207,138 +246,160 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 }
 
 // ------------------------------------------------------------------ QP core
-// Barrier terms of slot ls: hg[0..2] Hessian additions, hg[3..5] gradient additions.
-// corrector: c_j = sigma_mu - dt_aff dl_aff  (0 for the predictor)
-template <int S>
-__device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p, Stage<S>& st, int ls,
-                                              bool corrector, double smu) {
+// Barrier terms of slot ls into LDS: hg[0..2] Hessian additions, hg[3..5] gradient
+// additions.  Corrector: c_j = sigma_mu - dt_aff dl_aff (predictor: c_j = 0).
+template <int S, bool CORR>
+__device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls, double smu) {
     const int k = kof<S>(c, ls);
     double lo[3], hi[3];
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const bool act = (k < c.N) && (j > 0 || k >= 1);
-        const double tl = st.t[ls][2 * j], th = st.t[ls][2 * j + 1];
-        const double ll = st.lm[ls][2 * j], lh = st.lm[ls][2 * j + 1];
-        const double sl = ll / tl, sh = lh / th;
-        double cl = 0.0, ch = 0.0;
-        if (corrector) {
-            const double v = st.va[ls][j];
+        const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
+        const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
+        const double rtl = 1.0 / tl, rth = 1.0 / th;
+        const double sl = ll * rtl, sh = lh * rth;
+        double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
+        if (CORR) {
+            const double v = st.f(F_VA, ls, j);
             const double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
             const double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
-            cl = smu - dtl * dll;
-            ch = smu - dth * dlh;
+            const double cl = smu - dtl * dll, ch = smu - dth * dlh;
+            gadd += ch * rth - cl * rtl;
         }
-        const double hadd = sl + sh;
-        const double gadd = ((-sl * lo[j] - sh * hi[j]) + (lh - ll)) + (ch / th - cl / tl);
-        st.hg[ls][j] = act ? hadd : 0.0;
-        st.hg[ls][3 + j] = act ? gadd : 0.0;
+        st.hg(ls, j) = act ? sl + sh : 0.0;
+        st.hg(ls, 3 + j) = act ? gadd : 0.0;
     }
 }
 
-// slack/multiplier directions of slot ls from the bounded components v of a QP solution
-template <int S>
-__device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
-                                           const double v[3], bool corrector, double smu,
-                                           double dt[6], double dl[6]) {
+// Slack/multiplier directions of slot ls from the bounded components of a QP
+// solution (field VSRC), folded into the step-length bound: the largest alpha with
+// t + alpha dt >= 0 and l + alpha dl >= 0 is tracked as a ratio num/den without
+// dividing (den > 0).  UPDATE: apply t += alpha dt, l += alpha dl instead.
+template <int S, bool CORR>
+__device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls, int vsrc,
+                                           double smu, double& num, double& den, double& mu_aff_part, double alpha_aff,
+                                           bool update, double alpha) {
     const int k = kof<S>(c, ls);
     double lo[3], hi[3];
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const bool act = (k < c.N) && (j > 0 || k >= 1);
-        const double tl = st.t[ls][2 * j], th = st.t[ls][2 * j + 1];
-        const double ll = st.lm[ls][2 * j], lh = st.lm[ls][2 * j + 1];
-        const double sl = ll / tl, sh = lh / th;
-        double cl = 0.0, ch = 0.0;
-        if (corrector) {
-            const double va = st.va[ls][j];
+        const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
+        const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
+        const double rtl = 1.0 / tl, rth = 1.0 / th;
+        const double sl = ll * rtl, sh = lh * rth;
+        const double v = st.f(vsrc, ls, j);
+        double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
+        double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
+        if (CORR) {
+            const double va = st.f(F_VA, ls, j);
             const double atl = va - lo[j] - tl, ath = hi[j] - va - th;
             const double all = -ll - sl * atl, alh = -lh - sh * ath;
-            cl = smu - atl * all;
-            ch = smu - ath * alh;
+            dll += (smu - atl * all) * rtl;
+            dlh += (smu - ath * alh) * rth;
         }
-        const double dtl = v[j] - lo[j] - tl, dth = hi[j] - v[j] - th;
-        dt[2 * j] = act ? dtl : 0.0;
-        dt[2 * j + 1] = act ? dth : 0.0;
-        dl[2 * j] = act ? (cl / tl - ll - sl * dtl) : 0.0;
-        dl[2 * j + 1] = act ? (ch / th - lh - sh * dth) : 0.0;
+        dtl = act ? dtl : 0.0; dth = act ? dth : 0.0;
+        dll = act ? dll : 0.0; dlh = act ? dlh : 0.0;
+        if (update) {
+            st.t(ls, 2 * j) = tl + alpha * dtl;
+            st.t(ls, 2 * j + 1) = th + alpha * dth;
+            st.lm(ls, 2 * j) = ll + alpha * dll;
+            st.lm(ls, 2 * j + 1) = lh + alpha * dlh;
+        } else {
+            // ratio test: candidate t/(-dt) replaces num/den when t * den < num * (-dt)
+            if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
+            if (dth < 0.0 && th * den < num * -dth) { num = th; den = -dth; }
+            if (dll < 0.0 && ll * den < num * -dll) { num = ll; den = -dll; }
+            if (dlh < 0.0 && lh * den < num * -dlh) { num = lh; den = -dlh; }
+            if (!CORR) mu_aff_part += (tl + alpha_aff * dtl) * (ll + alpha_aff * dll) +
+                                      (th + alpha_aff * dth) * (lh + alpha_aff * dlh);
+        }
     }
-}
-
-__device__ __forceinline__ double max_step(double t, double dt, double l, double dl, double amax) {
-    if (dt < 0.0) amax = fmin(amax, -t / dt);
-    if (dl < 0.0) amax = fmin(amax, -l / dl);
-    return amax;
 }
 
 // Backward pass over the group (factorisation or vector only), then forward pass
-// writing the bounded components of the solution into `out` (va or vn).
+// writing the bounded components of the solution into LDS field `out` (F_VA / F_VN).
 template <int S, bool FACTOR>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
-                                              double (*out)[3]) {
+                                              int out) {
     double P[10], pv[4];
 #pragma unroll
     for (int i = 0; i < 10; ++i) P[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[i] = 0.0;
-    for (int j = c.L - 1; j >= 0; --j) {
-        if (c.lig == j) {
+    // Branch-free walk: every lane evaluates the step on its own slot data; only the
+    // lane whose turn it is (lig == j) keeps its factors, and only its chain value is
+    // consumed by the neighbour after the hand-over.  The terminal stage k = N sits in
+    // slot N % S of the last lane; the walk starts there.
+    const int lsN = c.N - (c.L - 1) * S;
 #pragma unroll
-            for (int ls = S - 1; ls >= 0; --ls) {
-                const int k = j * S + ls;
-                if (k == c.N) {
-                    if (FACTOR) ric_terminal(p, st.g[ls], P, pv);
-                    else {
+    for (int ls = 0; ls < S; ++ls) {
+        if (ls == lsN) {
+            if (FACTOR) ric_terminal(p, st.g[ls], P, pv);
+            else {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) pv[i] = st.g[ls][i];
-                    }
-                } else if (k < c.N) {
-                    const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], st.g[ls][3] + st.hg[ls][3]};
-                    const double gu[2] = {st.g[ls][4] + st.hg[ls][4], st.g[ls][5] + st.hg[ls][5]};
-                    if (FACTOR) {
-                        const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg[ls][0]};
-                        const double Hu[2] = {p.tau * p.W[4] + st.hg[ls][1], p.tau * p.W[5] + st.hg[ls][2]};
-                        ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, P, pv,
-                                        st.K[ls], st.Ri[ls], st.Pb[ls], st.kk[ls]);
-                    } else {
-                        ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Ri[ls], st.Pb[ls], pv, st.kk[ls]);
-                    }
-                }
+                for (int i = 0; i < 4; ++i) pv[i] = st.g[ls][i];
             }
+        }
+    }
+    for (int j = c.L - 1; j >= 0; --j) {
+        const bool act = (c.lig == j);
+#pragma unroll
+        for (int ls = S - 1; ls >= 0; --ls) {
+            if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
+            const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], st.g[ls][3] + st.hg(ls, 3)};
+            const double gu[2] = {st.g[ls][4] + st.hg(ls, 4), st.g[ls][5] + st.hg(ls, 5)};
+            double K[8], Ri[3], Pb[4], kk[2];
+            if (FACTOR) {
+                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg(ls, 0)};
+                const double Hu[2] = {p.tau * p.W[4] + st.hg(ls, 1), p.tau * p.W[5] + st.hg(ls, 2)};
+                ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, P, pv, K, Ri, Pb, kk);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st.K[ls][q] = act ? K[q] : st.K[ls][q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) st.Ri[ls][q] = act ? Ri[q] : st.Ri[ls][q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.Pb[ls][q] = act ? Pb[q] : st.Pb[ls][q];
+            } else {
+                ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Ri[ls], st.Pb[ls], pv, kk);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) st.kk[ls][q] = act ? kk[q] : st.kk[ls][q];
         }
         if (FACTOR) {
 #pragma unroll
-            for (int i = 0; i < 10; ++i) P[i] = __shfl_down(P[i], 1);
+            for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i]);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pv[i] = __shfl_down(pv[i], 1);
+        for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i]);
     }
-    // forward
+    // forward: every slot of lanes 0 .. L-2 is a stage k < N; the last lane holds lsN of them
     double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
     for (int j = 0; j < c.L; ++j) {
-        if (c.lig == j) {
+        const bool act = (c.lig == j);
 #pragma unroll
-            for (int ls = 0; ls < S; ++ls) {
-                const int k = j * S + ls;
-                if (k < c.N) {
-                    double du[2];
-                    du[0] = st.kk[ls][0] + (st.K[ls][0] * dx[0] + st.K[ls][1] * dx[1] + st.K[ls][2] * dx[2] + st.K[ls][3] * dx[3]);
-                    du[1] = st.kk[ls][1] + (st.K[ls][4] * dx[0] + st.K[ls][5] * dx[1] + st.K[ls][6] * dx[2] + st.K[ls][7] * dx[3]);
-                    out[ls][0] = dx[3];
-                    out[ls][1] = du[0];
-                    out[ls][2] = du[1];
-                    dyn_step(st.a[ls], st.B[ls], st.bb[ls], du, dx);
-                }
+        for (int ls = 0; ls < S; ++ls) {
+            if (j == c.L - 1 && ls >= lsN) continue;
+            double du[2];
+            du[0] = st.kk[ls][0] + (st.K[ls][0] * dx[0] + st.K[ls][1] * dx[1] + st.K[ls][2] * dx[2] + st.K[ls][3] * dx[3]);
+            du[1] = st.kk[ls][1] + (st.K[ls][4] * dx[0] + st.K[ls][5] * dx[1] + st.K[ls][6] * dx[2] + st.K[ls][7] * dx[3]);
+            if (act) {
+                st.f(out, ls, 0) = dx[3];
+                st.f(out, ls, 1) = du[0];
+                st.f(out, ls, 2) = du[1];
             }
+            dyn_step(st.a[ls], st.B[ls], st.bb[ls], du, dx);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dx[i] = __shfl_up(dx[i], 1);
+        for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i]);
     }
 }
 
 // Mehrotra predictor-corrector IPM on the current linearisation.  Leaves the
-// damped control step in st.du and the slacks/multipliers in st.t / st.lm.
+// damped control step in LDS (F_DU) and the slacks/multipliers in F_T / F_LM.
 // Returns the number of iterations taken by this lane's instance.
 template <int S>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4]) {
@@ -353,13 +414,13 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int j = 0; j < 3; ++j) {
             const bool act = (k < c.N) && (j > 0 || k >= 1);
             const double tl = fmax(-lo[j], p.t_min), th = fmax(hi[j], p.t_min);
-            st.t[ls][2 * j] = act ? tl : 1.0;
-            st.t[ls][2 * j + 1] = act ? th : 1.0;
-            st.lm[ls][2 * j] = act ? p.mu0 / tl : 0.0;
-            st.lm[ls][2 * j + 1] = act ? p.mu0 / th : 0.0;
+            st.t(ls, 2 * j) = act ? tl : 1.0;
+            st.t(ls, 2 * j + 1) = act ? th : 1.0;
+            st.lm(ls, 2 * j) = act ? p.mu0 / tl : 0.0;
+            st.lm(ls, 2 * j + 1) = act ? p.mu0 / th : 0.0;
         }
-        st.du[ls][0] = 0.0;
-        st.du[ls][1] = 0.0;
+        st.du(ls, 0) = 0.0;
+        st.du(ls, 1) = 0.0;
     }
     int nit = 0;
     for (int it = 0; it < p.qp_iters; ++it) {
@@ -367,62 +428,50 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
         for (int ls = 0; ls < S; ++ls)
 #pragma unroll
-            for (int q = 0; q < 6; ++q) tl_sum += st.t[ls][q] * st.lm[ls][q];
+            for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.base, c.L) / m;
         const bool done = !(mu >= p.mu_stop);
         if (__ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
         // ---- predictor
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls, false, 0.0);
-        riccati_solve<S, true>(c, p, st, dx0, st.va);
-        double amax = 1.0;
-        double dts[S][6], dls[S][6];
+        for (int ls = 0; ls < S; ++ls) barrier_terms<S, false>(c, p, st, ls, 0.0);
+        riccati_solve<S, true>(c, p, st, dx0, F_VA);
+        double num = 1.0, den = 1.0, dummy = 0.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            directions<S>(c, p, st, ls, st.va[ls], false, 0.0, dts[ls], dls[ls]);
-#pragma unroll
-            for (int q = 0; q < 6; ++q) amax = max_step(st.t[ls][q], dts[ls][q], st.lm[ls][q], dls[ls][q], amax);
-        }
-        const double aa = group_min(amax, c.base, c.L);
+        for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, dummy, 0.0, false, 0.0);
+        const double aa = group_min(num / den, c.base, c.L);
         double ma = 0.0;
+        num = 1.0; den = 1.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) ma += (st.t[ls][q] + aa * dts[ls][q]) * (st.lm[ls][q] + aa * dls[ls][q]);
+        for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, ma, aa, false, 0.0);
         const double mua = group_sum(ma, c.base, c.L) / m;
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
         const double smu = sg * mu;
         // ---- corrector
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls, true, smu);
-        riccati_solve<S, false>(c, p, st, dx0, st.vn);
-        double amx = 1.0 / p.frac;
+        for (int ls = 0; ls < S; ++ls) barrier_terms<S, true>(c, p, st, ls, smu);
+        riccati_solve<S, false>(c, p, st, dx0, F_VN);
+        num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            directions<S>(c, p, st, ls, st.vn[ls], true, smu, dts[ls], dls[ls]);
-#pragma unroll
-            for (int q = 0; q < 6; ++q) amx = max_step(st.t[ls][q], dts[ls][q], st.lm[ls][q], dls[ls][q], amx);
-        }
-        double alpha = p.frac * group_min(amx, c.base, c.L);
+        for (int ls = 0; ls < S; ++ls) directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, false, 0.0);
+        double alpha = p.frac * group_min(num / den, c.base, c.L);
         alpha = fmin(alpha, 1.0);
         if (done) alpha = 0.0;
+        // update (directions are recomputed from the same inputs before t, l change)
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                st.t[ls][q] += alpha * dts[ls][q];
-                st.lm[ls][q] += alpha * dls[ls][q];
-            }
-            st.du[ls][0] += alpha * (st.vn[ls][1] - st.du[ls][0]);
-            st.du[ls][1] += alpha * (st.vn[ls][2] - st.du[ls][1]);
+            const double vu0 = st.f(F_VN, ls, 1), vu1 = st.f(F_VN, ls, 2);
+            directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, true, alpha);
+            st.du(ls, 0) += alpha * (vu0 - st.du(ls, 0));
+            st.du(ls, 1) += alpha * (vu1 - st.du(ls, 1));
         }
     }
     return nit;
 }
 
-// State step of the damped QP solution (rollout of the affine dynamics), into st.dx.
+// State step of the damped QP solution (rollout of the affine dynamics), into LDS F_DX.
 template <int S>
 __device__ __forceinline__ void qp_rollout(const Ctx& c, Stage<S>& st, const double dx0[4]) {
     double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
@@ -433,13 +482,16 @@ __device__ __forceinline__ void qp_rollout(const Ctx& c, Stage<S>& st, const dou
                 const int k = j * S + ls;
                 if (k <= c.N) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) st.dx[ls][i] = dx[i];
+                    for (int i = 0; i < 4; ++i) st.dxs(ls, i) = dx[i];
                 }
-                if (k < c.N) dyn_step(st.a[ls], st.B[ls], st.bb[ls], st.du[ls], dx);
+                if (k < c.N) {
+                    const double du[2] = {st.du(ls, 0), st.du(ls, 1)};
+                    dyn_step(st.a[ls], st.B[ls], st.bb[ls], du, dx);
+                }
             }
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dx[i] = __shfl_up(dx[i], 1);
+        for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i]);
     }
 }
 
@@ -456,7 +508,7 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
                 const int k = j * S + ls;
                 if (k == c.N) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) pi[i] = p.We[i] * st.dx[ls][i] + st.g[ls][i];
+                    for (int i = 0; i < 4; ++i) pi[i] = p.We[i] * st.dxs(ls, i) + st.g[ls][i];
                 } else if (k < c.N) {
                     if (write && (!shift || k >= 1)) {
 #pragma unroll
@@ -469,12 +521,12 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
                     if (k >= 1) {
                         const double* a = st.a[ls];
                         double np[4];
-                        np[0] = p.tau * p.W[0] * st.dx[ls][0] + st.g[ls][0] + pi[0];
-                        np[1] = p.tau * p.W[1] * st.dx[ls][1] + st.g[ls][1] + pi[1];
-                        np[2] = p.tau * p.W[2] * st.dx[ls][2] + st.g[ls][2] + (a[0] * pi[0] + a[2] * pi[1] + pi[2]);
-                        np[3] = p.tau * p.W[3] * st.dx[ls][3] + st.g[ls][3] +
+                        np[0] = p.tau * p.W[0] * st.dxs(ls, 0) + st.g[ls][0] + pi[0];
+                        np[1] = p.tau * p.W[1] * st.dxs(ls, 1) + st.g[ls][1] + pi[1];
+                        np[2] = p.tau * p.W[2] * st.dxs(ls, 2) + st.g[ls][2] + (a[0] * pi[0] + a[2] * pi[1] + pi[2]);
+                        np[3] = p.tau * p.W[3] * st.dxs(ls, 3) + st.g[ls][3] +
                                 (a[1] * pi[0] + a[3] * pi[1] + a[4] * pi[2] + a[5] * pi[3]);
-                        np[3] += st.lm[ls][1] - st.lm[ls][0];
+                        np[3] += st.lm(ls, 1) - st.lm(ls, 0);
 #pragma unroll
                         for (int i = 0; i < 4; ++i) pi[i] = np[i];
                     }
@@ -482,74 +534,98 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
             }
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pi[i] = __shfl_down(pi[i], 1);
+        for (int i = 0; i < 4; ++i) pi[i] = wave_from_next(pi[i]);
     }
-}
-
-// ------------------------------------------------------------- linearisation
-template <int S>
-__device__ __forceinline__ void linearize(const Ctx& c, const SolveParams& p, const ShapeDev& sh, Stage<S>& st,
-                                          const double* yref, const double* yref_e) {
-    // x_{k+1} of the last slot lives in slot 0 of the next lane
-    double xnext[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xnext[i] = __shfl_down(st.x[0][i], 1);
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        double xn1[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xn1[i] = (ls + 1 < S) ? st.x[(ls + 1 < S) ? ls + 1 : 0][i] : xnext[i];
-        if (k < c.N) {
-            Lin L;
-            rk4<true>(sh, p.Ts, st.x[ls], st.u[ls], L);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) st.bb[ls][i] = L.xn[i] - xn1[i];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) st.a[ls][i] = L.a[i];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) st.B[ls][i] = L.B[i];
-            const double* yr = yref + (size_t)k * 6;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) st.g[ls][i] = p.tau * p.W[i] * (st.x[ls][i] - yr[i]);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) st.g[ls][4 + i] = p.tau * p.W[4 + i] * (st.u[ls][i] - yr[4 + i]);
-        } else if (k == c.N) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) st.g[ls][i] = p.We[i] * (st.x[ls][i] - yref_e[i]);
-            st.g[ls][4] = st.g[ls][5] = 0.0;
-        }
-    }
-}
-
-template <int S>
-__device__ __forceinline__ double stage_cost(const Ctx& c, const SolveParams& p, const Stage<S>& st,
-                                             const double* yref, const double* yref_e) {
-    double cost = 0.0;
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        if (k < c.N) {
-            const double* yr = yref + (size_t)k * 6;
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { const double r = st.x[ls][i] - yr[i]; s += p.W[i] * r * r; }
-#pragma unroll
-            for (int i = 0; i < 2; ++i) { const double r = st.u[ls][i] - yr[4 + i]; s += p.W[4 + i] * r * r; }
-            cost += 0.5 * p.tau * s;
-        } else if (k == c.N) {
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { const double r = st.x[ls][i] - yref_e[i]; s += p.We[i] * r * r; }
-            cost += 0.5 * s;
-        }
-    }
-    return cost;
 }
 
 // ------------------------------------------------------------------ kernels
+// One solve = prologue, K x (linearize, qp), epilogue; all on one stream.
+// Workspace (SolveArgs::w*): SQP iterate X/U, wrapped x0, stage data in SoA.
+enum LinField : int { L_A = 0, L_B = 6, L_BB = 14, L_G = 18, L_COUNT = 24 };
+
+// NMPC_controller.solve prologue (NMPC_controller.m:332-384) or acados-level init copy.
+__global__ void prologue_kernel(SolveArgs A) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.B) return;
+    const SolveParams& p = A.p;
+    const int N = p.N;
+    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
+    double x0[4];
+    for (int c = 0; c < 4; ++c) x0[c] = A.x0[(size_t)i * 4 + c];
+    double* X = A.wX + (size_t)i * (N + 1) * 4;
+    double* U = A.wU + (size_t)i * N * 2;
+    A.qp_iter[i] = 0;
+    if (!(A.flags & QSP_FLAG_CONTROLLER)) {
+        for (int q = 0; q < (N + 1) * 4; ++q) X[q] = A.X_in[(size_t)i * (N + 1) * 4 + q];
+        for (int q = 0; q < N * 2; ++q) U[q] = A.U_in[(size_t)i * N * 2 + q];
+        for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
+        return;
+    }
+    x0[3] = mat_mod(x0[3], sh.b) - sh.b * ((x0[3] < 0.0) ? 1.0 : 0.0);   // :332
+    for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
+    const bool cold = (A.warm_valid == nullptr || A.warm_valid[i] == 0);
+    for (int k = 0; k < N; ++k) {                                            // :351-355
+        U[2 * k] = cold ? p.cp.u_n_lb : A.U_in[((size_t)i * N + k) * 2];
+        U[2 * k + 1] = cold ? 0.0 : A.U_in[((size_t)i * N + k) * 2 + 1];
+    }
+    double xc[4] = {x0[0], x0[1], x0[2], x0[3]};
+    for (int k = 0; k <= N; ++k) {                                           // :357-380
+        for (int c = 0; c < 4; ++c) X[4 * k + c] = xc[c];
+        if (k == N) break;
+        const double vb = v_bound(sh, p.cp, xc[3]);
+        const double ut_old = U[2 * k + 1];
+        if (fabs(ut_old) > vb) {
+            const double sgn = ut_old > 0.0 ? 1.0 : -1.0;
+            U[2 * k + 1] = sgn * vb;
+            U[2 * k] = U[2 * k + 1] * U[2 * k] / ut_old;
+        }
+        DynOut d;
+        dynamics<false>(sh, xc[2], xc[3], U[2 * k], U[2 * k + 1], d);
+        for (int c = 0; c < 4; ++c) xc[c] = xc[c] + p.Ts * d.f[c];
+    }
+}
+
+// Stage-parallel linearisation: one thread per (instance, stage k = 0..N).
+__global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
+    const SolveParams& p = A.p;
+    const int N = p.N;
+    const size_t tot = (size_t)A.B * (N + 1);
+    const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= tot) return;
+    const int i = (int)(gi / (N + 1)), k = (int)(gi - (size_t)i * (N + 1));
+    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
+    const double* X = A.wX + (size_t)i * (N + 1) * 4;
+    double* out = A.wlin + gi;
+    if (k < N) {
+        const double xk[4] = {X[4 * k], X[4 * k + 1], X[4 * k + 2], X[4 * k + 3]};
+        const double uk[2] = {A.wU[((size_t)i * N + k) * 2], A.wU[((size_t)i * N + k) * 2 + 1]};
+        Lin L;
+        rk4<true>(sh, p.Ts, xk, uk, L);
+        const double* yr = A.yref + ((size_t)i * N + k) * 6;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) out[(L_A + q) * tot] = L.a[q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) out[(L_B + q) * tot] = L.B[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(L_BB + q) * tot] = L.xn[q] - X[4 * (k + 1) + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(L_G + q) * tot] = p.tau * p.W[q] * (xk[q] - yr[q]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) out[(L_G + 4 + q) * tot] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
+    } else {
+        const double* ye = A.yref_e + (size_t)i * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(L_G + q) * tot] = p.We[q] * (X[4 * N + q] - ye[q]);
+        out[(L_G + 4) * tot] = 0.0;
+        out[(L_G + 5) * tot] = 0.0;
+    }
+}
+
+// The QP of one SQP iteration in the register/LDS-resident lane-group layout:
+// load stage data, Mehrotra IPM, roll out the damped step, update the SQP iterate.
 template <int S>
-__global__ void __launch_bounds__(256) sqp_kernel(SolveArgs A) {
+__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int last) {
+    extern __shared__ double smem[];
     const SolveParams& p = A.p;
     Ctx c;
     c.lane = threadIdx.x & 63;
@@ -564,125 +640,104 @@ __global__ void __launch_bounds__(256) sqp_kernel(SolveArgs A) {
     c.real = (c.grp < G) && (c.inst < A.B);
     const int iv = c.real ? c.inst : A.B - 1;
     const int N = p.N;
-
-    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[iv] : 0];
+    const size_t tot = (size_t)A.B * (N + 1);
     Stage<S> st;
-
-    // ---------------- inputs: x0, references, initial guess
-    double x0[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x0[i] = A.x0[(size_t)iv * 4 + i];
-    const bool ctrl = (A.flags & QSP_FLAG_CONTROLLER) != 0;
-    if (ctrl) x0[3] = mat_mod(x0[3], sh.b) - sh.b * ((x0[3] < 0.0) ? 1.0 : 0.0);   // NMPC_controller.m:332
-    const double* yref = A.yref + (size_t)iv * N * 6;
-    const double* yref_e = A.yref_e + (size_t)iv * 4;
-    const bool cold = ctrl && (A.warm_valid == nullptr || A.warm_valid[iv] == 0);
+    st.lds = smem + threadIdx.x;
+    double* X = A.wX + (size_t)iv * (N + 1) * 4;
+    double* U = A.wU + (size_t)iv * N * 2;
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
         const int kc = k <= N ? k : N;
         const int ku = k < N ? k : N - 1;
+        const double* in = A.wlin + (size_t)iv * (N + 1) + kc;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st.x[ls][i] = cold ? 0.0 : A.X_in[((size_t)iv * (N + 1) + kc) * 4 + i];
-        st.u[ls][0] = cold ? p.cp.u_n_lb : A.U_in[((size_t)iv * N + ku) * 2 + 0];   // :351-355
-        st.u[ls][1] = cold ? 0.0 : A.U_in[((size_t)iv * N + ku) * 2 + 1];
+        for (int q = 0; q < 6; ++q) st.a[ls][q] = in[(L_A + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st.B[ls][q] = in[(L_B + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st.bb[ls][q] = in[(L_BB + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) st.g[ls][q] = in[(L_G + q) * tot];
+        st.v(ls, 0) = X[4 * kc + 3];
+        st.v(ls, 1) = U[2 * ku];
+        st.v(ls, 2) = U[2 * ku + 1];
     }
-    if (ctrl) {
-        // :357-380  clip + Euler warm-start rollout, serial along the horizon
-        double xc[4] = {x0[0], x0[1], x0[2], x0[3]};
-        for (int j = 0; j < c.L; ++j) {
-            if (c.lig == j) {
+    double dx0[4];
 #pragma unroll
-                for (int ls = 0; ls < S; ++ls) {
-                    const int k = j * S + ls;
-                    if (k <= N) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) st.x[ls][i] = xc[i];
-                    }
-                    if (k < N) {
-                        const double vb = v_bound(sh, p.cp, xc[3]);
-                        const double ut_old = st.u[ls][1];
-                        if (fabs(ut_old) > vb) {
-                            const double sgn = ut_old > 0.0 ? 1.0 : -1.0;
-                            st.u[ls][1] = sgn * vb;
-                            st.u[ls][0] = st.u[ls][1] * st.u[ls][0] / ut_old;
-                        }
-                        DynOut d;
-                        dynamics<false>(sh, xc[2], xc[3], st.u[ls][0], st.u[ls][1], d);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) xc[i] = xc[i] + p.Ts * d.f[i];
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) xc[i] = __shfl_up(xc[i], 1);
-        }
-    }
-
-    // ---------------- SQP
-    int status = 0;
-    int qp_total = 0;
-    for (int it = 0; it < p.sqp_iters; ++it) {
-        linearize<S>(c, p, sh, st, yref, yref_e);
-        double dx0[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dx0[i] = x0[i] - st.x[0][i];   // valid in lane lig == 0
-        qp_total += qp_ipm<S>(c, p, st, dx0);
-        qp_rollout<S>(c, st, dx0);
-        const bool last = (it + 1 == p.sqp_iters);
-        if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, (A.flags & QSP_FLAG_SHIFT) != 0);
+    for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
+    const int nit = qp_ipm<S>(c, p, st, dx0);
+    qp_rollout<S>(c, st, dx0);
+    if (A.qp_dx) {
+        // QP-level interface (qsp_qp_solve): report the QP solution itself
+        if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, false);
+        if (!c.real) return;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
             const int k = kof<S>(c, ls);
-            if (k <= N) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) st.x[ls][i] += st.dx[ls][i];
-            }
+            if (k <= N)
+                for (int q = 0; q < 4; ++q) A.qp_dx[((size_t)iv * (N + 1) + k) * 4 + q] = st.dxs(ls, q);
             if (k < N) {
-                st.u[ls][0] += st.du[ls][0];
-                st.u[ls][1] += st.du[ls][1];
+                for (int q = 0; q < 2; ++q) A.qp_du[((size_t)iv * N + k) * 2 + q] = st.du(ls, q);
+                for (int q = 0; q < 6; ++q) A.qp_lam[((size_t)iv * N + k) * 6 + q] = st.lm(ls, q);
             }
+            if (k == 0) A.qp_iter[iv] = nit;
         }
+        return;
     }
-    // ---------------- outputs
-    bool bad = false;
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        if (k <= N) for (int i = 0; i < 4; ++i) bad |= !isfinite(st.x[ls][i]);
-        if (k < N) for (int i = 0; i < 2; ++i) bad |= !isfinite(st.u[ls][i]);
-    }
-    const double nbad = group_sum(bad ? 1.0 : 0.0, c.base, c.L);
-    status = nbad > 0.0 ? 1 : 0;
-    const double cost = group_sum(stage_cost<S>(c, p, st, yref, yref_e), c.base, c.L);
+    if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, (A.flags & QSP_FLAG_SHIFT) != 0);
     if (!c.real) return;
-    const bool shift = (A.flags & QSP_FLAG_SHIFT) != 0;
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
-        if (k == 0) {
-            A.u0[(size_t)iv * 2 + 0] = st.u[ls][0];
-            A.u0[(size_t)iv * 2 + 1] = st.u[ls][1];
-            A.status[iv] = status;
-            A.sqp_iter[iv] = p.sqp_iters;
-            A.qp_iter[iv] = qp_total;
-            A.cost[iv] = cost;
-        }
-        if (k <= N) {
-            // shifted: X(:,k-1) = X(:,k) for k>=1, and X(:,N) = X(:,N)  (NMPC_controller.m:397-399)
-            if (!shift || k >= 1)
-                for (int i = 0; i < 4; ++i) A.X_out[((size_t)iv * (N + 1) + (shift ? k - 1 : k)) * 4 + i] = st.x[ls][i];
-            if (shift && k == N)
-                for (int i = 0; i < 4; ++i) A.X_out[((size_t)iv * (N + 1) + N) * 4 + i] = st.x[ls][i];
-        }
+        if (k <= N)
+            for (int q = 0; q < 4; ++q) X[4 * k + q] += st.dxs(ls, q);
         if (k < N) {
-            if (!shift || k >= 1)
-                for (int i = 0; i < 2; ++i) A.U_out[((size_t)iv * N + (shift ? k - 1 : k)) * 2 + i] = st.u[ls][i];
-            if (shift && k == N - 1)
-                for (int i = 0; i < 2; ++i) A.U_out[((size_t)iv * N + N - 1) * 2 + i] = st.u[ls][i];
+            U[2 * k] += st.du(ls, 0);
+            U[2 * k + 1] += st.du(ls, 1);
         }
+        if (k == 0) A.qp_iter[iv] += nit;
     }
-    if (A.warm_valid && ctrl) A.warm_valid[iv] = 1;
+}
+
+// status, cost, u0 and the (optionally shifted, NMPC_controller.m:397-399) outputs.
+__global__ void epilogue_kernel(SolveArgs A) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.B) return;
+    const SolveParams& p = A.p;
+    const int N = p.N;
+    const double* X = A.wX + (size_t)i * (N + 1) * 4;
+    const double* U = A.wU + (size_t)i * N * 2;
+    const double* yref = A.yref + (size_t)i * N * 6;
+    const double* ye = A.yref_e + (size_t)i * 4;
+    bool bad = false;
+    double cost = 0.0;
+    for (int k = 0; k < N; ++k) {
+        double s = 0.0;
+        for (int q = 0; q < 4; ++q) { const double r = X[4 * k + q] - yref[6 * k + q]; s += p.W[q] * r * r; bad |= !isfinite(X[4 * k + q]); }
+        for (int q = 0; q < 2; ++q) { const double r = U[2 * k + q] - yref[6 * k + 4 + q]; s += p.W[4 + q] * r * r; bad |= !isfinite(U[2 * k + q]); }
+        cost += 0.5 * p.tau * s;
+    }
+    double s = 0.0;
+    for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s += p.We[q] * r * r; bad |= !isfinite(X[4 * N + q]); }
+    cost += 0.5 * s;
+    A.cost[i] = cost;
+    A.status[i] = bad ? 1 : 0;
+    A.sqp_iter[i] = p.sqp_iters;
+    A.u0[(size_t)i * 2] = U[0];
+    A.u0[(size_t)i * 2 + 1] = U[1];
+    const int sh = (A.flags & QSP_FLAG_SHIFT) ? 1 : 0;
+    double* Xo = A.X_out + (size_t)i * (N + 1) * 4;
+    double* Uo = A.U_out + (size_t)i * N * 2;
+    for (int k = 0; k <= N; ++k) {
+        const int src = (k + sh <= N) ? k + sh : N;
+        for (int q = 0; q < 4; ++q) Xo[4 * k + q] = X[4 * src + q];
+    }
+    for (int k = 0; k < N; ++k) {
+        const int src = (k + sh < N) ? k + sh : N - 1;
+        for (int q = 0; q < 2; ++q) Uo[2 * k + q] = U[2 * src + q];
+    }
+    if (A.warm_valid && (A.flags & QSP_FLAG_CONTROLLER)) A.warm_valid[i] = 1;
 }
 
 // ----------------------------------------------------- building-block kernels
@@ -737,106 +792,51 @@ __global__ void vbound_kernel(const ShapeDev* shapes, const int32_t* sid, int n,
     vb[i] = v_bound(shapes[sid[i]], cp, s[i]);
 }
 
-// Batched LQ-QP solve with given stage data (QP-level parity).  Uses the same
-// register-resident lane layout and IPM as the SQP kernel.  A must have the
-// pusher-slider structure (only its six free entries are read).
-template <int S>
-__global__ void __launch_bounds__(256) qp_kernel(QPArgs A) {
-    const SolveParams& p = A.p;
-    Ctx c;
-    c.lane = threadIdx.x & 63;
-    c.N = p.N;
-    c.L = (p.N + S) / S;
-    const int G = 64 / c.L;
-    c.grp = c.lane / c.L;
-    c.lig = c.lane - c.grp * c.L;
-    c.base = c.grp * c.L;
-    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    c.inst = wave * G + c.grp;
-    c.real = (c.grp < G) && (c.inst < A.nb);
-    const int iv = c.real ? c.inst : A.nb - 1;
-    const int N = p.N;
-    Stage<S> st;
-    // bounds in step space: lo = lh - v, hi = uh - v  =>  v = lh - lo  (QPArgs uses lh = 0)
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        const int ku = k < N ? k : N - 1;
-        const double* Ak = A.A + ((size_t)iv * N + ku) * 16;
-        st.a[ls][0] = Ak[2]; st.a[ls][1] = Ak[3]; st.a[ls][2] = Ak[6];
-        st.a[ls][3] = Ak[7]; st.a[ls][4] = Ak[11]; st.a[ls][5] = Ak[15];
-        for (int q = 0; q < 8; ++q) st.B[ls][q] = A.B[((size_t)iv * N + ku) * 8 + q];
-        for (int q = 0; q < 4; ++q) st.bb[ls][q] = A.b[((size_t)iv * N + ku) * 4 + q];
-        const double* gk = A.g + (size_t)iv * (6 * N + 4) + (k < N ? 6 * k : 6 * N);
-        for (int q = 0; q < 6; ++q) st.g[ls][q] = (k < N || q < 4) ? gk[q] : 0.0;
-        // encode the bounds through x/u so that bnd_lohi() reproduces lo/hi with lh = 0
-        const double* lo = A.lo + ((size_t)iv * N + ku) * 3;
-        st.x[ls][3] = -lo[0]; st.u[ls][0] = -lo[1]; st.u[ls][1] = -lo[2];
-    }
-    // lo = lh - v with lh = 0 and hi = uh - v with uh = bound width (equal on every stage, as in the OCP);
-    // Hessian: tau = 1, W = stage diag, We = terminal diag (equal on every stage, as in the OCP).
-    SolveParams pq = p;
-    for (int j = 0; j < 3; ++j) { pq.lh[j] = 0.0; pq.uh[j] = A.width[j]; }
-    double dx0[4];
-    for (int i = 0; i < 4; ++i) dx0[i] = A.dx0[(size_t)iv * 4 + i];
-    const int nit = qp_ipm<S>(c, pq, st, dx0);
-    qp_rollout<S>(c, st, dx0);
-    qp_adjoint_store<S>(c, pq, st, A.pi + (size_t)iv * N * 4, c.real, false);
-    if (!c.real) return;
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        if (k <= N) for (int i = 0; i < 4; ++i) A.dx[((size_t)iv * (N + 1) + k) * 4 + i] = st.dx[ls][i];
-        if (k < N) {
-            for (int i = 0; i < 2; ++i) A.du[((size_t)iv * N + k) * 2 + i] = st.du[ls][i];
-            for (int q = 0; q < 6; ++q) A.lam[((size_t)iv * N + k) * 6 + q] = st.lm[ls][q];
-        }
-        if (k == 0) A.iters[iv] = nit;
-    }
-}
-
 // ------------------------------------------------------------------ launchers
 template <int S>
-static hipError_t launch_sqp_S(const SolveArgs& a, hipStream_t stream) {
+static hipError_t launch_qp_step(const SolveArgs& a, int last, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.B + G - 1) / G;
-    const int threads = 256;
-    const int blocks = (waves * 64 + threads - 1) / threads;
-    hipLaunchKernelGGL(sqp_kernel<S>, dim3(blocks), dim3(threads), 0, stream, a);
+    const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)qp_step_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_bytes<S>());
+        attr = true;
+    }
+    hipLaunchKernelGGL(qp_step_kernel<S>, dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, last);
     return hipGetLastError();
 }
 
-template <int S>
-static hipError_t launch_qp_S(const QPArgs& a, hipStream_t stream) {
-    const int L = (a.p.N + S) / S;
-    const int G = 64 / L;
-    const int waves = (a.nb + G - 1) / G;
-    const int threads = 256;
-    const int blocks = (waves * 64 + threads - 1) / threads;
-    hipLaunchKernelGGL(qp_kernel<S>, dim3(blocks), dim3(threads), 0, stream, a);
-    return hipGetLastError();
+static hipError_t launch_qp_any(const SolveArgs& a, int S, int last, hipStream_t stream) {
+    switch (S) {
+        case 1: return launch_qp_step<1>(a, last, stream);
+        case 2: return launch_qp_step<2>(a, last, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 int lanes_per_instance(int N, int S) { return (N + S) / S; }
 
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream) {
-    switch (S) {
-        case 1: return launch_sqp_S<1>(a, stream);
-        case 2: return launch_sqp_S<2>(a, stream);
-        case 3: return launch_sqp_S<3>(a, stream);
-        default: return hipErrorInvalidValue;
+    const unsigned gb = (unsigned)((a.B + 127) / 128);
+    hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    const size_t tot = (size_t)a.B * (a.p.N + 1);
+    const unsigned gl = (unsigned)((tot + 255) / 256);
+    for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
+        hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = launch_qp_any(a, S, it + 1 == a.p.sqp_iters, stream);
     }
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(epilogue_kernel, dim3(gb), dim3(128), 0, stream, a);
+    return hipGetLastError();
 }
 
-hipError_t launch_qp(const QPArgs& a, int S, hipStream_t stream) {
-    switch (S) {
-        case 1: return launch_qp_S<1>(a, stream);
-        case 2: return launch_qp_S<2>(a, stream);
-        case 3: return launch_qp_S<3>(a, stream);
-        default: return hipErrorInvalidValue;
-    }
-}
+// One QP (qsp_qp_solve): the workspace already holds the stage data.
+hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) { return launch_qp_any(a, S, 1, stream); }
 
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream) {
