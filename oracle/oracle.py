@@ -140,9 +140,10 @@ class Oracle:
         du = np.zeros((nb, N, 2))
         pi = np.zeros((nb, N, 4))
         lam = np.zeros((nb, N, 6))
+        iters = np.zeros(nb, np.int32)
         r = self.L.or_qp_batch(C.byref(opts), C.c_int32(nb), *[_p(a) for a in arrs], _p(act), _p(dx0),
-                               _p(dx), _p(du), _p(pi), _p(lam))
-        return dict(dx=dx, du=du, pi=pi, lam=lam, fail=r)
+                               _p(dx), _p(du), _p(pi), _p(lam), _p(iters))
+        return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters, fail=r)
 
     def ocp_solve(self, opts, x0, yref, yref_e, X=None, U=None, PI=None, shape_id=None, nthreads=0):
         N = opts.N
@@ -157,10 +158,12 @@ class Oracle:
         lam = np.zeros((nb, N, 6))
         status = np.zeros(nb, np.int32)
         iters = np.zeros(nb, np.int32)
+        qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
         self.L.or_ocp_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
-                            _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(cost), C.c_int(nthreads))
-        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, cost=cost)
+                            _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(qp_iter), _p(cost),
+                            C.c_int(nthreads))
+        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
 
     def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0):
         """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place."""
@@ -173,11 +176,13 @@ class Oracle:
         u0 = np.zeros((nb, 2))
         status = np.zeros(nb, np.int32)
         iters = np.zeros(nb, np.int32)
+        qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
         self.L.or_controller_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
                                    C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]),
-                                   _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(cost), C.c_int(nthreads))
-        return dict(u0=u0, status=status, iters=iters, cost=cost)
+                                   _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(qp_iter), _p(cost),
+                                   C.c_int(nthreads))
+        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
 
     @staticmethod
     def new_warm(nb, N):

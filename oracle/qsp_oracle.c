@@ -414,7 +414,7 @@ static inline double bnd_val(const double *dx, const double *du, int k, int j)
 }
 
 /* Mehrotra predictor-corrector IPM.  Returns 0 on success, 1 on NaN. */
-static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, double *work)
+static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, double *work, int *nit_out)
 {
     int N = qp->N;
     double *Hd = work, *gd = work + 6 * N, *dxn = work + 12 * N, *dun = dxn + 4 * (N + 1);
@@ -436,11 +436,13 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     for (int k = 0; k < N; ++k) { sol->du[2 * k] = 0.0; sol->du[2 * k + 1] = 0.0; }
     static const int comp[3] = {3, 4, 5};
 
+    int nit = 0;
     for (int it = 0; it < o->qp_iters; ++it) {
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
         mu /= (double)m;
         if (mu < o->mu_stop) break;
+        nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
             if (pass == 1) {
@@ -500,6 +502,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < 2; ++i) sol->du[2 * k + i] += alpha * (dun[2 * k + i] - sol->du[2 * k + i]);
     }
+    if (nit_out) *nit_out = nit;
     /* final state rollout from the damped controls */
     double x[4];
     memcpy(x, qp->dx0, sizeof x);
@@ -548,6 +551,7 @@ typedef struct {
     double lam[OR_MAX_N * 6], t[OR_MAX_N * 6];
     double work[OR_MAX_N * 40 + 64];
     or_fact F;
+    int qp_total;
 } or_ws;
 
 static double ocp_cost(const or_opts *o, int N, const double *X, const double *U, const double *yref, const double *yref_e)
@@ -672,7 +676,9 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 break;
             }
         }
-        if (qp_solve(&qp, o, &sol, &ws->F, ws->work)) { status = 1; break; }
+        int nit = 0;
+        if (qp_solve(&qp, o, &sol, &ws->F, ws->work, &nit)) { status = 1; ws->qp_total += nit; break; }
+        ws->qp_total += nit;
         double alpha = 1.0;
         if (o->nlp_mode == 1) {
             /* merit weights (acados: max(|mult|, (weight + |mult|)/2)) */
@@ -789,7 +795,7 @@ int or_vbound(const int32_t *n_ctrl, const double *ctrl, const double *knots, co
  * Outputs dx ((N+1)x4), du (N x 2), pi (N x 4), lam (N x 6). */
 int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, const double *b,
                 const double *H, const double *g, const double *lo, const double *hi, const uint8_t *act,
-                const double *dx0, double *dx, double *du, double *pi, double *lam)
+                const double *dx0, double *dx, double *du, double *pi, double *lam, int32_t *iters)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -807,7 +813,7 @@ int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, 
             memcpy(qp.dx0, dx0 + 4 * i, sizeof qp.dx0);
             or_qp_sol sol = {dx + (size_t)i * 4 * (N + 1), du + (size_t)i * 2 * N, pi + (size_t)i * 4 * N,
                              lam + (size_t)i * 6 * N, ws->t};
-            if (qp_solve(&qp, o, &sol, &ws->F, ws->work)) {
+            if (qp_solve(&qp, o, &sol, &ws->F, ws->work, iters ? iters + i : NULL)) {
                 #pragma omp atomic write
                 fail = 1;
             }
@@ -823,7 +829,8 @@ int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, 
 int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
                  int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
                  const double *x0, const double *yref, const double *yref_e,
-                 double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, double *cost, int nthreads)
+                 double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
+                 double *cost, int nthreads)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -838,7 +845,9 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
             or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
             double *Xi = X + (size_t)i * 4 * (N + 1), *Ui = U + (size_t)i * 2 * N, *Pi = PI + (size_t)i * 4 * N;
             const double *yr = yref + (size_t)i * 6 * N, *ye = yref_e + (size_t)i * 4;
+            ws->qp_total = 0;
             status[i] = sqp_solve(&sh, o, x0 + 4 * i, yr, ye, Xi, Ui, Pi, lam ? lam + (size_t)i * 6 * N : NULL, iters ? iters + i : NULL, ws);
+            if (qp_iter) qp_iter[i] = ws->qp_total;
             cost[i] = ocp_cost(o, N, Xi, Ui, yr, ye);
         }
         free(ws);
@@ -855,7 +864,7 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                         int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
                         const double *x0_in, const double *traj, int32_t T, const int32_t *index_time,
                         double *Xw, double *Uw, double *PIw, uint8_t *warm_valid,
-                        double *u0, int32_t *status, int32_t *iters, double *cost, int nthreads)
+                        double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -909,7 +918,9 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                 }
             }
             /* :389 solve */
+            ws->qp_total = 0;
             status[i] = sqp_solve(&sh, o, x0, yref, ye, X, U, PI, NULL, iters ? iters + i : NULL, ws);
+            if (qp_iter) qp_iter[i] = ws->qp_total;
             cost[i] = ocp_cost(o, N, X, U, yref, ye);
             u0[2 * i] = U[0]; u0[2 * i + 1] = U[1];
             /* :397-399 shift (duplicate last column) */

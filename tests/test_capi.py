@@ -1,0 +1,109 @@
+"""CPU: the HIP library loads, exports every entry point of include/qsp_nmpc.h, its
+host-side pieces (PLY preprocessing, option/argument validation) behave, and the
+ctypes mirrors of the C structs have the header's layout.  No kernel is launched."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "qsp_nmpc.h")
+
+
+def _header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(qsp_[A-Za-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from uclv_qs_pushing_matlab_amd import _lib
+    L = _lib.lib()
+    names = _header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTED), set(names) ^ set(_lib.EXPORTED)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    from uclv_qs_pushing_matlab_amd import _lib
+    src = tmp_path / "sz.c"
+    src.write_text('#include "qsp_nmpc.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(qsp_options), sizeof(qsp_shape),'
+                   ' sizeof(qsp_device_io), offsetof(qsp_shape, b), offsetof(qsp_device_io, warm_valid));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    want = [C.sizeof(_lib.Options), C.sizeof(_lib.Shape), C.sizeof(_lib.DeviceIO),
+            _lib.Shape.b.offset, _lib.DeviceIO.warm_valid.offset]
+    assert got == want
+
+
+def test_default_options_and_validation():
+    from uclv_qs_pushing_matlab_amd import _lib
+    L = _lib.lib()
+    o = _lib.Options()
+    L.qsp_default_options(C.byref(o))
+    assert (o.N, o.batch, o.sqp_iters, o.Ts, o.cost_scale_Ts) == (20, 1, 50, 0.05, 1)
+    h = C.c_void_p()
+    bad = _lib.Options()
+    L.qsp_default_options(C.byref(bad))
+    bad.N = 0
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1          # QSP_ERR_ARG before any HIP call
+    assert b"N and batch" in L.qsp_last_error()
+    bad.N, bad.Ts = 20, 0.0
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    bad.Ts, bad.stages_per_lane = 0.05, 7
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    bad.stages_per_lane, bad.nlp_mode = 0, 5
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    assert L.qsp_solve(None) == -1
+
+
+def test_shape_from_ply_matches_oracle_bitwise():
+    """Product-side contour preprocessing (C++, qsp_shape_from_ply) vs the oracle's numpy restatement."""
+    from oracle.shapes_np import load_object
+    from uclv_qs_pushing_matlab_amd.objects import make_shape, object_selection
+    for name in ("santal", "balea", "montana", "pulirapid"):
+        sh = make_shape(name)
+        o = load_object(name)
+        n = sh.n_ctrl
+        assert n == len(o["P"])
+        P = np.array([[sh.ctrl[i][0], sh.ctrl[i][1]] for i in range(n)])
+        np.testing.assert_array_equal(P, o["P"])
+        np.testing.assert_array_equal(np.array(sh.knots[:n + 4]), o["S"])
+        assert sh.b == o["b"] and sh.c_ellipse == o["c"] and sh.mu_sp == o["mu"]
+        assert object_selection(name)["mu_sp"] == sh.mu_sp
+
+
+def test_shape_from_ply_errors(tmp_path):
+    from uclv_qs_pushing_matlab_amd import _lib
+    L = _lib.lib()
+    sh = _lib.Shape()
+    assert L.qsp_shape_from_ply(str(tmp_path / "missing.ply").encode(), 0, 0.3, 0.2, 0.3, 0.02, C.byref(sh)) == -4
+    bad = tmp_path / "ascii.ply"
+    bad.write_text("ply\nformat ascii 1.0\nelement vertex 3\nproperty float x\nproperty float y\nend_header\n0 0\n1 0\n0 1\n")
+    assert L.qsp_shape_from_ply(str(bad).encode(), 0, 0.3, 0.2, 0.3, 0.02, C.byref(sh)) == -4
+
+
+def test_no_cpu_fallback(monkeypatch):
+    """The product path fails loudly when the HIP library is missing."""
+    from uclv_qs_pushing_matlab_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libqsp_nmpc.so")
+    with pytest.raises(_lib.QspError):
+        _lib.lib()
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "uclv_qs_pushing_matlab_amd")
+    pat = re.compile(r"^\s*(from\s+oracle|import\s+oracle)|qsp_oracle|libqsp_oracle", re.M)
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")):
+                assert not pat.search(open(os.path.join(dirpath, f)).read()), f

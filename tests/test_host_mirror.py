@@ -1,0 +1,37 @@
+"""CPU: host-side mirrors of the reference interfaces (no kernel launches)."""
+import numpy as np
+import pytest
+
+from uclv_qs_pushing_matlab_amd.objects import OBJECT_NAMES, object_selection
+from uclv_qs_pushing_matlab_amd.trajectory import TrajectoryGenerator
+
+
+def test_object_selection_values():
+    s = object_selection("santal")                      # object_selection.m:3-12
+    assert (s["mu_sg"], s["mu_sp"], s["m"], s["tau_max"]) == (0.32, 0.19, 0.2875, 0.0251)
+    assert abs(s["area"] - 0.068 * 0.082) < 1e-15
+    assert set(OBJECT_NAMES) == {"santal", "balea", "montana", "pulirapid"}
+    with pytest.raises(ValueError):
+        object_selection("unknown")
+
+
+def test_straight_line_quintic():
+    tg = TrajectoryGenerator(0.05, 0.01)                # TrajectoryGenerator.m:44-79
+    tg.set_target(np.zeros(4), np.array([0.3, 0.03, 0.2, 0.0]), 0.0, 10.0)
+    t, traj = tg.straight_line(False)
+    assert len(t) == 201 and traj.shape == (4, 201)
+    np.testing.assert_allclose(traj[:, 0], 0.0, atol=1e-15)
+    np.testing.assert_allclose(traj[:, -1], [0.3, 0.03, 0.2, 0.0], atol=1e-12)
+    v = np.diff(traj[0])
+    assert np.all(v >= -1e-15) and abs(v[0]) < 1e-6      # zero initial velocity (quintic)
+
+
+def test_waypoints_config1_is_linear():
+    tg = TrajectoryGenerator(0.05, 0.01)                # main.m:150-164
+    tg.set_target(np.zeros(4), np.zeros(5), 0.0, 10.0)
+    tg.waypoints_ = np.array([[0, 0, 0], [0.10, 0, 0]])
+    tg.waypoints_velocities = [0.010]
+    t, traj = tg.waypoints_gen()
+    assert len(t) == 201
+    np.testing.assert_allclose(traj[0], 0.01 * t, atol=1e-15)
+    np.testing.assert_allclose(traj[1:], 0.0, atol=1e-15)

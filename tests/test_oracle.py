@@ -1,0 +1,221 @@
+"""CPU: the oracle against the committed golden fixtures, the reference's data files,
+the survey-time values derived from them, and mathematical invariants.
+
+Parity against acados is UNPINNED (acados/CasADi/MATLAB are not runnable here); these
+checks pin the oracle to what can be pinned."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, config2_x0, straight_traj
+from oracle.oracle import make_opts
+from oracle.shapes_np import load_object
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+def test_shape_tables_match_golden():
+    gold = json.load(open(os.path.join(GOLDEN, "shapes.json")))
+    for n in NAMES:
+        o = load_object(n)
+        g = gold[n]
+        assert len(o["P"]) == g["n"]
+        np.testing.assert_array_equal(o["P"], np.array(g["P"]))
+        np.testing.assert_array_equal(o["S"], np.array(g["S"]))
+        assert o["b"] == g["b"] and o["c"] == g["c"] and o["mu"] == g["mu"]
+
+
+def test_shape_values_from_reference_data():
+    # control points, knot counts, contour lengths, c_ellipse
+    expect = {"santal": (37, 0.281899, 0.027811, 0.19), "balea": (37, 0.222486, 0.0071409, 0.20),
+              "montana": (35, 0.285079, 0.020867, 0.10), "pulirapid": (56, 0.596013, 0.023260, 0.10)}
+    for n, (nc, b, c, mu) in expect.items():
+        o = load_object(n)
+        assert len(o["P"]) == nc and len(o["S"]) == nc + 4
+        assert abs(o["b"] - b) < 5e-7 and abs(o["c"] - c) / c < 5e-5 and o["mu"] == mu
+        np.testing.assert_array_equal(o["P"][0], o["P"][-1])          # closed contour
+        assert np.all(np.diff(o["S"]) >= 0) and o["S"][0] == 0 and o["S"][-1] == o["b"]
+
+
+def test_santal_contact_geometry(oracle):
+    # C(0) = (-0.031, 0.024463), t(0) = (0, 1), gamma_l = 0.7176, gamma_r = 0.3492
+    C, dC, D, dD, kap = oracle.spline([0.0], 0)
+    np.testing.assert_allclose(C[0], [-0.031, 0.024463], atol=5e-7)
+    t = D[0] / np.linalg.norm(D[0])
+    np.testing.assert_allclose(t, [0.0, 1.0], atol=1e-12)
+    # pure pushing at s = 0 is slide-right: s_dot = -gamma_r u_n
+    f, _ = oracle.dynamics([[0, 0, 0, 0]], [[0.01, 0.0]], 0)
+    assert abs(-f[0, 3] / 0.01 - 0.3492) < 5e-4
+
+
+def test_spline_invariants(oracle):
+    for sid, n in enumerate(NAMES):
+        o = load_object(n)
+        C, dC, D, dD, _ = oracle.spline([0.0, o["b"]], sid)
+        np.testing.assert_allclose(C[0], o["P"][0], atol=1e-15)     # C(0) = P_1 (clamped)
+        assert np.all(C[1] == 0.0) and np.all(D[1] == 0.0)           # C(b) = 0: half-open indicator
+        s = np.linspace(0, o["b"], 400, endpoint=False)
+        C, dC, D, dD, _ = oracle.spline(s, sid)
+        np.testing.assert_allclose(dC, D, rtol=1e-9, atol=1e-9)      # d/ds FC == FC_dot
+        # the derivative of FC_dot agrees with a central difference away from knots
+        h = 1e-7
+        Cp = oracle.spline(s + h, sid)[2]
+        Cm = oracle.spline(s - h, sid)[2]
+        fd = (Cp - Cm) / (2 * h)
+        knots = np.asarray(o["S"])
+        far = np.min(np.abs(s[:, None] - knots[None, :]), axis=1) > 1e-5
+        np.testing.assert_allclose(dD[far], fd[far], rtol=1e-5, atol=1e-4)
+
+
+def test_dynamics_invariants(oracle):
+    rng = np.random.default_rng(0)
+    for sid, n in enumerate(NAMES):
+        b = load_object(n)["b"]
+        x = np.stack([rng.uniform(-.1, .1, 200), rng.uniform(-.1, .1, 200), rng.uniform(-3, 3, 200),
+                      rng.uniform(-b, b, 200)], 1)
+        f, J = oracle.dynamics(x, np.zeros((200, 2)), sid)
+        assert np.all(f == 0.0) and np.all(J == 0.0)                 # rho = 0/0: no mode active
+        u = np.stack([rng.uniform(1e-3, .03, 200), rng.uniform(-.05, .05, 200)], 1)
+        f, J = oracle.dynamics(x, u, sid)
+        assert np.all(J[:, :, :2] == 0.0)                            # f independent of (x, y)
+        assert np.all(J[:, 2:, 2] == 0.0)                            # theta_dot, s_dot independent of theta
+        # forward-mode AD vs central differences (away from mode switches)
+        h = 1e-7
+        for c in range(6):
+            dx = np.zeros((200, 4)); du = np.zeros((200, 2))
+            (dx if c < 4 else du)[:, c % 4 if c < 4 else c - 4] = h
+            fp, _ = oracle.dynamics(x + dx, u + du, sid)
+            fm, _ = oracle.dynamics(x - dx, u - du, sid)
+            fd = (fp - fm) / (2 * h)
+            # drop points whose mode changes inside the stencil (Jacobian jumps there)
+            ok = np.all(np.abs(fd - J[:, :, c]) < 1e-5 * (1 + np.abs(J[:, :, c])), axis=1)
+            assert ok.mean() > 0.97, (n, c, ok.mean())
+
+
+def test_motion_cone_continuity(oracle):
+    # f is continuous across the cone edges rho = gamma_l and rho = gamma_r:
+    # locate each edge by bisection on the sticking indicator (s_dot == 0 exactly while
+    # sticking) and check that f does not jump there
+    x = np.array([[0.0, 0.0, 0.1, 0.03]])
+    un = 0.01
+
+    def f_at(rho):
+        return oracle.dynamics(x, [[un, un * rho]], sid)[0][0]
+
+    for sid in range(4):
+        for lo, hi in ((0.0, 50.0), (0.0, -50.0)):
+            assert f_at(lo)[3] == 0.0 or f_at(hi)[3] != 0.0
+            if f_at(lo)[3] != 0.0:
+                continue                      # rho = 0 already sliding for this shape/point
+            for _ in range(200):
+                mid = 0.5 * (lo + hi)
+                if f_at(mid)[3] == 0.0:
+                    lo = mid
+                else:
+                    hi = mid
+            jump = np.abs(f_at(hi) - f_at(lo)).max()
+            assert jump < 1e-9, (sid, lo, hi, jump)
+
+
+def test_rk4_sensitivities_vs_fd(oracle):
+    rng = np.random.default_rng(1)
+    x = np.stack([rng.uniform(-.05, .05, 100), rng.uniform(-.05, .05, 100), rng.uniform(-1, 1, 100),
+                  rng.uniform(-.05, .05, 100)], 1)
+    u = np.stack([rng.uniform(1e-3, .03, 100), rng.uniform(-.05, .05, 100)], 1)
+    xn, A, B = oracle.rk4(x, u, 0.05, 0)
+    h = 1e-7
+    for c in range(6):
+        dx = np.zeros((100, 4)); du = np.zeros((100, 2))
+        (dx if c < 4 else du)[:, c if c < 4 else c - 4] = h
+        fp = oracle.rk4(x + dx, u + du, 0.05, 0)[0]
+        fm = oracle.rk4(x - dx, u - du, 0.05, 0)[0]
+        fd = (fp - fm) / (2 * h)
+        an = A[:, :, c] if c < 4 else B[:, :, c - 4]
+        ok = np.all(np.abs(fd - an) < 1e-5 * (1 + np.abs(an)), axis=1)
+        assert ok.mean() > 0.95
+
+
+def test_model_points_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "model_points.npz"))
+    f, J = oracle.dynamics(g["x"], g["u"], g["sid"])
+    np.testing.assert_array_equal(f, g["f"])
+    np.testing.assert_array_equal(J, g["J"])
+    xn, A, B = oracle.rk4(g["x"], g["u"], 0.05, g["sid"])
+    np.testing.assert_array_equal(xn, g["xn"])
+    np.testing.assert_array_equal(A, g["A"])
+    C, dC, D, dD, kap = oracle.spline(g["sigma"], g["sid"])
+    np.testing.assert_array_equal(C, g["C"])
+    np.testing.assert_array_equal(kap, g["kappa"])
+
+
+def test_qp_kkt(oracle):
+    from qp_data import build_qp
+    N, nb = 20, 32
+    op = make_opts(N=N, sqp_iters=3)
+    x0 = config2_x0(nb, 5)
+    traj = straight_traj()
+    yref = np.repeat(traj[None, :N], nb, 0)
+    yref_e = yref[:, N - 1, :4].copy()
+    r = oracle.ocp_solve(op, x0, yref, yref_e, X=np.repeat(x0[:, None], N + 1, 1))
+    A, B, b, H, g, lo, hi, act, dx0 = build_qp(oracle, op, r["X"], r["U"], yref, yref_e, x0)
+    s = oracle.qp(op, A, B, b, H, g, lo, hi, act, dx0)
+    assert s["fail"] == 0
+    conv = s["iters"] < op.qp_iters            # QPs that met mu < mu_stop within the cap
+    assert conv.mean() > 0.9
+    for i in np.where(conv)[0]:
+        dx, du, pi, lam = s["dx"][i], s["du"][i], s["pi"][i], s["lam"][i]
+        np.testing.assert_allclose(dx[0], dx0[i], atol=1e-15)
+        for k in range(N):
+            # dynamics
+            np.testing.assert_allclose(dx[k + 1], A[i, k] @ dx[k] + B[i, k] @ du[k] + b[i, k], atol=1e-12)
+            # bounds (IPM: interior up to the final barrier parameter)
+            v = np.array([dx[k, 3], du[k, 0], du[k, 1]])
+            sl = slice(0 if k >= 1 else 1, 3)
+            assert np.all(v[sl] >= lo[i, k, sl] - 1e-8) and np.all(v[sl] <= hi[i, k, sl] + 1e-8)
+            # stationarity w.r.t. u_k
+            rs = H[i, 6 * k + 4:6 * k + 6] * du[k] + g[i, 6 * k + 4:6 * k + 6] + B[i, k].T @ pi[k] \
+                - lam[k, 2::2] + lam[k, 3::2]
+            scale = 1 + np.abs(B[i, k].T @ pi[k]).max()
+            # IPM accuracy at mu_stop = 1e-10: the u_t directions carry only tau*W_u = 5e-5 of
+            # curvature, so barrier-level residuals (mu/t) stay visible
+            assert np.abs(rs).max() < 1e-3 * scale, (i, k, rs)
+
+
+def test_config1_closed_loop_golden(oracle):
+    gold = json.load(open(os.path.join(GOLDEN, "config1_closed_loop.json")))
+    traj = straight_traj()
+    for N in (10, 20):
+        op = make_opts(N=N, sqp_iters=5)
+        warm = oracle.new_warm(1, N)
+        xs = np.zeros((1, 4))
+        for i in range(1, 21):
+            r = oracle.controller_solve(op, xs, traj, i, warm)
+            np.testing.assert_allclose(r["u0"][0], gold[f"N{N}"]["u0"][i - 1], rtol=0, atol=1e-12)
+            fx, _ = oracle.dynamics(xs, r["u0"])
+            xs = xs + 0.05 * fx
+        np.testing.assert_allclose(xs[0], gold[f"N{N}"]["x_final"], atol=1e-12)
+        # the slider follows the 0.01 m/s reference: x(1 s) ~ 0.010 m
+        assert abs(xs[0, 0] - 0.01) < 2e-3
+
+
+def test_config2_batch_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "config2_batch64.npz"))
+    N = 20
+    r = oracle.controller_solve(make_opts(N=N, sqp_iters=50), g["x0"], straight_traj(), 1,
+                                oracle.new_warm(len(g["x0"]), N))
+    st = g["stable"]
+    np.testing.assert_allclose(r["u0"][st], g["u0"][st], atol=1e-12)
+    assert np.all(r["status"] == 0)
+    assert np.all(g["u0"][:, 0] >= -1e-9) and np.all(g["u0"][:, 0] <= 0.03 + 1e-9)      # u_n bounds
+    assert np.all(np.abs(g["u0"][:, 1]) <= 0.05 + 1e-9)                                  # u_t bounds
+
+
+def test_vbound_definition(oracle):
+    op = make_opts()
+    s = np.linspace(-0.3, 0.3, 301)
+    vb = oracle.vbound(s, op, 0)
+    kap = oracle.spline(np.mod(s, load_object("santal")["b"]), 0)[4]
+    ref = np.minimum(1.0 / (np.abs(np.abs(kap) - 3.0) + 1e-4), 0.05)
+    np.testing.assert_allclose(vb, ref, rtol=1e-12)

@@ -28,15 +28,24 @@
 namespace qsp {
 
 // ------------------------------------------------------------- group helpers
+// Reductions over the L lanes of an instance group: a log-step tree towards the
+// group's first lane, then a broadcast, so every lane of the group holds the same
+// value (identical decisions in all lanes of an instance).
 __device__ __forceinline__ double group_sum(double v, int base, int L) {
-    double s = 0.0;
-    for (int d = 0; d < L; ++d) s += __shfl(v, base + d);   // fixed order: identical in every lane
-    return s;
+    const int lig = (int)(threadIdx.x & 63) - base;
+    for (int off = 1; off < L; off <<= 1) {
+        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
+        v += (lig + off < L) ? o : 0.0;
+    }
+    return __shfl(v, base);
 }
 __device__ __forceinline__ double group_min(double v, int base, int L) {
-    double s = v;
-    for (int d = 0; d < L; ++d) s = fmin(s, __shfl(v, base + d));
-    return s;
+    const int lig = (int)(threadIdx.x & 63) - base;
+    for (int off = 1; off < L; off <<= 1) {
+        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
+        v = (lig + off < L) ? fmin(v, o) : v;
+    }
+    return __shfl(v, base);
 }
 
 // symmetric 4x4 stored as 10 entries: (0,0)(0,1)(0,2)(0,3)(1,1)(1,2)(1,3)(2,2)(2,3)(3,3)
@@ -59,7 +68,8 @@ enum LdsField : int {
     F_VN = 20,    // 3  corrector bounded components
     F_DX = 23,    // 4  final QP state step
     F_HG = 27,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
-    F_COUNT = 33
+    F_RT = 33,    // 6  1 / slack, refreshed whenever the slacks change
+    F_COUNT = 39
 };
 template <int S>
 constexpr int lds_bytes() { return F_COUNT * S * BLOCK * 8; }
@@ -79,6 +89,7 @@ struct Stage {
     __device__ __forceinline__ double& du(int ls, int i) const { return f(F_DU, ls, i); }
     __device__ __forceinline__ double& dxs(int ls, int i) const { return f(F_DX, ls, i); }
     __device__ __forceinline__ double& hg(int ls, int i) const { return f(F_HG, ls, i); }
+    __device__ __forceinline__ double& rt(int ls, int q) const { return f(F_RT, ls, q); }
 };
 
 struct Ctx {
@@ -258,7 +269,7 @@ __device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p
         const bool act = (k < c.N) && (j > 0 || k >= 1);
         const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
-        const double rtl = 1.0 / tl, rth = 1.0 / th;
+        const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
         const double sl = ll * rtl, sh = lh * rth;
         double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
         if (CORR) {
@@ -289,7 +300,7 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
         const bool act = (k < c.N) && (j > 0 || k >= 1);
         const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
-        const double rtl = 1.0 / tl, rth = 1.0 / th;
+        const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
         const double sl = ll * rtl, sh = lh * rth;
         const double v = st.f(vsrc, ls, j);
         double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
@@ -304,8 +315,11 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
         dtl = act ? dtl : 0.0; dth = act ? dth : 0.0;
         dll = act ? dll : 0.0; dlh = act ? dlh : 0.0;
         if (update) {
-            st.t(ls, 2 * j) = tl + alpha * dtl;
-            st.t(ls, 2 * j + 1) = th + alpha * dth;
+            const double tln = tl + alpha * dtl, thn = th + alpha * dth;
+            st.t(ls, 2 * j) = tln;
+            st.t(ls, 2 * j + 1) = thn;
+            st.rt(ls, 2 * j) = 1.0 / tln;
+            st.rt(ls, 2 * j + 1) = 1.0 / thn;
             st.lm(ls, 2 * j) = ll + alpha * dll;
             st.lm(ls, 2 * j + 1) = lh + alpha * dlh;
         } else {
@@ -414,10 +428,13 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int j = 0; j < 3; ++j) {
             const bool act = (k < c.N) && (j > 0 || k >= 1);
             const double tl = fmax(-lo[j], p.t_min), th = fmax(hi[j], p.t_min);
+            const double rl = 1.0 / tl, rh = 1.0 / th;
             st.t(ls, 2 * j) = act ? tl : 1.0;
             st.t(ls, 2 * j + 1) = act ? th : 1.0;
-            st.lm(ls, 2 * j) = act ? p.mu0 / tl : 0.0;
-            st.lm(ls, 2 * j + 1) = act ? p.mu0 / th : 0.0;
+            st.rt(ls, 2 * j) = act ? rl : 1.0;
+            st.rt(ls, 2 * j + 1) = act ? rh : 1.0;
+            st.lm(ls, 2 * j) = act ? p.mu0 * rl : 0.0;
+            st.lm(ls, 2 * j + 1) = act ? p.mu0 * rh : 0.0;
         }
         st.du(ls, 0) = 0.0;
         st.du(ls, 1) = 0.0;
