@@ -161,6 +161,8 @@ def main():
     torch.cuda.synchronize(dev)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events at every kernel boundary of the timed solves, recorded on the launch stream
+    solver.set_kernel_timing(args.steps)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -174,6 +176,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
+    ktimes = solver.kernel_times()
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -183,18 +186,22 @@ def main():
     qp_iter = solver.get("qp_iter")
     status = d_st.cpu().numpy()
     u0 = d_u0.cpu().numpy()
-    flops_launch = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())
+    flops_solve = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())   # all lanes, one solve
+    # dominant kernel: qp_step (one launch = one SQP iteration's QP for every lane of the shard)
+    qp_ms, qp_n = ktimes["qp_step"]
+    qp_avg_s = qp_ms / max(qp_n, 1) * 1e-3
+    qp_flops_launch = float(qp_iter.astype(np.float64).sum()) * N * FLOP_IPM_STAGE / K
     if dist:
-        tt = torch.tensor([flops_launch, float(np.count_nonzero(status))], dtype=torch.float64, device=dev)
+        tt = torch.tensor([float(np.count_nonzero(status))], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        flops_all, nbad = float(tt[0]), int(tt[1])
+        nbad = int(tt[0])
     else:
-        flops_all, nbad = flops_launch, int(np.count_nonzero(status))
+        nbad = int(np.count_nonzero(status))
 
     total_solves = B * world * args.steps
     value = total_solves / elapsed
     avg_kern_s = float(np.mean(kern_ms)) * 1e-3
-    achieved = flops_launch / avg_kern_s / 1e12
+    achieved = qp_flops_launch / qp_avg_s / 1e12
 
     result = {
         "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
@@ -208,10 +215,13 @@ def main():
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
         "status_nonzero_lanes": nbad,
-        "roofline": {"bound": "mfma", "peak_kind": "FP64 vector (= FP64 matrix) peak; the kernel is FP64-VALU bound",
+        "kernels_ms_avg": {k: (v[0] / v[1] if v[1] else None) for k, v in ktimes.items()},
+        "roofline": {"bound": "mfma", "kernel": "qp_step_kernel",
+                     "peak_kind": "FP64 vector (= FP64 matrix) dense peak; the kernel is FP64-VALU bound",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                     "flops_per_launch": flops_launch, "flops_per_solve_mean": flops_launch / Bl},
+                     "flops_per_launch": qp_flops_launch, "launch_ms_avg": qp_avg_s * 1e3,
+                     "whole_solve_tflops": flops_solve / avg_kern_s / 1e12},
     }
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -234,14 +244,18 @@ def main():
         u0_ref = r["u0"]
         d = np.abs(u0[:n] - u0_ref).max(1)
         m = min(n, 512)
-        rp = run(slice(0, m), x0[:m] * (1 + 1e-13))
-        stable = np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
+        # a lane is 'stable' when the oracle itself stays put (< 1e-9) under three 1e-13 relative
+        # perturbations of x0: the full-step SQP amplifies rounding on the other lanes
+        stable = np.ones(m, bool)
+        for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+            rp = run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13))
+            stable &= np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
         result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
                             "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
                             "stable_lanes": int(stable.sum()), "stable_checked": int(m),
                             "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
                             "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
-                                    "< 1e-9 under a 1e-13 relative perturbation of x0 (non-chaotic lane)"}
+                                    "< 1e-9 under three 1e-13 relative perturbations of x0 (non-chaotic lane)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -145,6 +145,13 @@ int qsp_controller_reset(qsp_solver* s);                                        
 /* ------------------------------------------------ device-resident fast path */
 int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* hip_stream);
 int qsp_synchronize(qsp_solver* s);
+/* Per-kernel timing (acados' time_lin / time_qp split).  qsp_set_kernel_timing(s, n) pre-creates
+ * HIP events for the next n solves (0 disables): every kernel boundary of each solve is then
+ * recorded on the solve's stream.  qsp_get_kernel_times synchronises the recorded events and
+ * returns the summed milliseconds and launch counts per kernel family in the order
+ * {prologue, linearize, qp_step, epilogue}, then re-arms the pool. */
+int qsp_set_kernel_timing(qsp_solver* s, int32_t max_solves);
+int qsp_get_kernel_times(qsp_solver* s, double* ms /* 4 */, int32_t* launches /* 4 */);
 
 /* ------------------------------------------- building blocks (host arrays) */
 int qsp_eval_spline(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* sigma,

@@ -1,20 +1,50 @@
-"""Summarise rocprofv3 --pmc CSV passes per kernel (developer tool)."""
+"""Summarise rocprofv3 --pmc CSV passes per kernel (developer tool) and, with --json,
+write the HBM traffic of the dominant kernel per launch (profiles/pmc_traffic.json,
+read by bench.py's roofline.traffic).
+
+Units/corrections (MI355X_MICROARCH.md, HBM section): rocprofv3's FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced read, so it is doubled; WRITE_SIZE is taken as is.
+"""
+import argparse
 import collections
 import csv
 import glob
-import sys
+import json
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+ap = argparse.ArgumentParser()
+ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
+ap.add_argument("--json", default=None)
+ap.add_argument("--kernel", default="qp_step_kernel")
+ap.add_argument("--batch", type=int, default=65536)
+ap.add_argument("--N", type=int, default=20)
+ap.add_argument("--sqp-iters", type=int, default=50)
+args = ap.parse_args()
+
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
-calls = collections.defaultdict(set)
-for f in sorted(glob.glob(f"{root}/p*/p*_counter_collection.csv")):
+ndisp = collections.defaultdict(lambda: collections.defaultdict(set))
+for f in sorted(glob.glob(f"{args.root}/p*/p*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        calls[k].add((f, r["Dispatch_Id"]))
+        ndisp[k][r["Counter_Name"]].add((f, r["Dispatch_Id"]))
 for k, d in tot.items():
     if "qsp" not in k:
         continue
     print(k)
     for c, v in sorted(d.items()):
-        print(f"   {c:28s} {v:.4e}")
+        n = len(ndisp[k][c])
+        print(f"   {c:28s} total {v:.4e}   per launch {v / n:.4e}  ({n} launches)")
+
+if args.json:
+    ks = [k for k in tot if args.kernel in k]
+    assert ks, f"no {args.kernel} dispatches"
+    fetch = sum(tot[k]["FETCH_SIZE"] for k in ks) / sum(len(ndisp[k]["FETCH_SIZE"]) for k in ks)
+    write = sum(tot[k]["WRITE_SIZE"] for k in ks) / sum(len(ndisp[k]["WRITE_SIZE"]) for k in ks)
+    rd, wr = fetch * 1024 * 2, write * 1024
+    out = {"kernel": args.kernel, "batch": args.batch, "N": args.N, "sqp_iters": args.sqp_iters,
+           "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+           "raw_FETCH_SIZE_KiB": fetch, "raw_WRITE_SIZE_KiB": write,
+           "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024"}
+    json.dump(out, open(args.json, "w"), indent=1)
+    print(json.dumps(out))

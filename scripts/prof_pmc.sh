@@ -1,9 +1,10 @@
 #!/bin/bash
-# PMC passes on the bench kernel (one --pmc group per pass; kernel-trace only, no sys/runtime trace)
+# PMC passes on the bench workload (one counter group per pass; --pmc with kernel trace only,
+# never with sys/runtime traces).  Summary -> $OUT/summary.txt and $OUT/pmc_traffic.json
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:-"--no-cpu --steps 1 --warmup 0 --batch 16384"}
+ARGS=${ARGS:-"--no-cpu --steps 1 --warmup 0"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
@@ -12,6 +13,7 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 S
            "SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o p$i -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/p$i -o p$i -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || exit $?
+  echo "pmc pass $i done"
 done
-echo pmc-done
+python scripts/pmc_summary.py $OUT --json $OUT/pmc_traffic.json > $OUT/summary.txt

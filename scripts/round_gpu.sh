@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU session: smoke, GPU parity tests, kernel-trace stats, PMC traffic, full bench.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+R=${R:-gpurun_out/round}
+mkdir -p $R
+export TMPDIR=/tmp
+echo "smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.log 2>&1 || { cat $R/smoke.log; exit 1; }
+tail -1 $R/smoke.log
+echo "gpu tests"
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > $R/tests.log 2>&1 || { tail -30 $R/tests.log; exit 1; }
+tail -2 $R/tests.log
+if [ -z "$SKIP_PROF" ]; then
+  echo "kernel trace"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/kt -o kt -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $R/kt_bench.json 2> $R/kt_bench.err || exit $?
+  echo "pmc"
+  OUT=$R/pmc bash scripts/prof_pmc.sh || exit $?
+  cp $R/pmc/pmc_traffic.json profiles/pmc_traffic.json
+fi
+echo "bench"
+timeout -k 10 900 python bench.py > $R/bench.json 2> $R/bench.err || { tail -20 $R/bench.err; exit 1; }
+cat $R/bench.json

@@ -107,3 +107,11 @@ def test_product_does_not_import_oracle():
         for f in files:
             if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")):
                 assert not pat.search(open(os.path.join(dirpath, f)).read()), f
+
+
+def test_mex_gateway_compiles():
+    """integration/matlab/qsp_nmpc_mex.c type-checks against the C ABI (MEX API from a
+    declaration-only stub; MATLAB is absent)."""
+    src = os.path.join(ROOT, "integration", "matlab", "qsp_nmpc_mex.c")
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "tests", "stubs"), src])

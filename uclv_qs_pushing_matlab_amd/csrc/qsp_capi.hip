@@ -60,9 +60,22 @@ struct qsp_solver {
     int32_t T = 0;
     bool have_traj = false;
     float last_ms = 0.0f;
+    std::vector<hipEvent_t> kev;   // kernel-timing pool (qsp_set_kernel_timing)
+    int kev_used = 0;
+    std::vector<int> kev_solves;   // event offset of each timed solve
 };
 
 // --------------------------------------------------------------- helpers
+// events for one timed solve (nullptr when timing is off or the pool is used up)
+static hipEvent_t* take_kernel_events(qsp_solver* s) {
+    const int per = 2 * s->o.sqp_iters + 3;
+    if (s->kev.empty() || s->kev_used + per > (int)s->kev.size()) return nullptr;
+    s->kev_solves.push_back(s->kev_used);
+    hipEvent_t* e = s->kev.data() + s->kev_used;
+    s->kev_used += per;
+    return e;
+}
+
 static void fill_params(qsp_solver* s) {
     SolveParams& p = s->p;
     p.N = s->o.N;
@@ -79,9 +92,9 @@ static void fill_params(qsp_solver* s) {
 }
 
 static int auto_S(int N) {
-    // Register-resident layout; S = 2 measured fastest at N = 20 (profiles/ROUND1.md).
-    (void)N;
-    return 2;
+    // Register-resident layout: one stage per lane is fastest at N = 20 (profiles/ROUND1.md:
+    // 234k vs 224k solves/s for S = 2); two stages per lane once N + 1 exceeds a wavefront.
+    return N + 1 <= 64 ? 1 : 2;
 }
 
 // Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
@@ -151,7 +164,7 @@ static SolveArgs make_args(qsp_solver* s) {
 
 static int run_timed(qsp_solver* s, const SolveArgs& a) {
     HIPCHK(hipEventRecord(s->ev0, s->stream));
-    HIPCHK(launch_sqp(a, s->S, s->stream));
+    HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s)));
     HIPCHK(hipEventRecord(s->ev1, s->stream));
     HIPCHK(hipEventSynchronize(s->ev1));
     HIPCHK(hipEventElapsedTime(&s->last_ms, s->ev0, s->ev1));
@@ -288,6 +301,7 @@ int qsp_destroy(qsp_solver* s) {
                       &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
+    for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -568,7 +582,44 @@ int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
         a.warm_valid = io->warm_valid;
     }
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    HIPCHK(launch_sqp(a, s->S, st));
+    HIPCHK(launch_sqp(a, s->S, st, take_kernel_events(s)));
+    return QSP_OK;
+}
+
+int qsp_set_kernel_timing(qsp_solver* s, int32_t max_solves) {
+    if (!s || max_solves < 0) return fail(QSP_ERR_ARG, "qsp_set_kernel_timing: bad argument");
+    HIPCHK(hipSetDevice(s->o.device));
+    for (hipEvent_t e : s->kev) HIPCHK(hipEventDestroy(e));
+    s->kev.clear();
+    s->kev_solves.clear();
+    s->kev_used = 0;
+    const size_t n = (size_t)max_solves * (2 * s->o.sqp_iters + 3);
+    for (size_t i = 0; i < n; ++i) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        s->kev.push_back(e);
+    }
+    return QSP_OK;
+}
+
+int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
+    if (!s || !ms || !launches) return fail(QSP_ERR_ARG, "qsp_get_kernel_times: null argument");
+    HIPCHK(hipSetDevice(s->o.device));
+    for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; }
+    const int K = s->o.sqp_iters;
+    for (int off : s->kev_solves) {
+        hipEvent_t* e = s->kev.data() + off;
+        HIPCHK(hipEventSynchronize(e[2 * K + 2]));
+        float t;
+        HIPCHK(hipEventElapsedTime(&t, e[0], e[1])); ms[0] += t; launches[0] += 1;
+        for (int it = 0; it < K; ++it) {
+            HIPCHK(hipEventElapsedTime(&t, e[1 + 2 * it], e[2 + 2 * it])); ms[1] += t; launches[1] += 1;
+            HIPCHK(hipEventElapsedTime(&t, e[2 + 2 * it], e[3 + 2 * it])); ms[2] += t; launches[2] += 1;
+        }
+        HIPCHK(hipEventElapsedTime(&t, e[2 * K + 1], e[2 * K + 2])); ms[3] += t; launches[3] += 1;
+    }
+    s->kev_solves.clear();
+    s->kev_used = 0;
     return QSP_OK;
 }
 

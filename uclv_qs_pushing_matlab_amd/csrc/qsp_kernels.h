@@ -44,7 +44,9 @@ struct SolveArgs {
 
 
 int lanes_per_instance(int N, int S);
-hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream);
+// ev (optional): 2*sqp_iters + 3 events recorded on `stream` at every kernel boundary
+// (prologue | linearize, qp_step x sqp_iters | epilogue), for per-kernel timing.
+hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream);

@@ -836,20 +836,29 @@ static hipError_t launch_qp_any(const SolveArgs& a, int S, int last, hipStream_t
 
 int lanes_per_instance(int N, int S) { return (N + S) / S; }
 
-hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream) {
+hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev) {
+    int ne = 0;
+    auto mark = [&]() { return ev ? hipEventRecord(ev[ne++], stream) : hipSuccess; };
     const unsigned gb = (unsigned)((a.B + 127) / 128);
+    hipError_t e = mark();
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess) e = mark();
     const size_t tot = (size_t)a.B * (a.p.N + 1);
     const unsigned gl = (unsigned)((tot + 255) / 256);
     for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
         hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
         e = hipGetLastError();
+        if (e == hipSuccess) e = mark();
         if (e == hipSuccess) e = launch_qp_any(a, S, it + 1 == a.p.sqp_iters, stream);
+        if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(epilogue_kernel, dim3(gb), dim3(128), 0, stream, a);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e == hipSuccess) e = mark();
+    return e;
 }
 
 // One QP (qsp_qp_solve): the workspace already holds the stage data.

@@ -217,6 +217,19 @@ class OcpSolver:
     def synchronize(self):
         check(self._L.qsp_synchronize(self._h), "qsp_synchronize")
 
+    def set_kernel_timing(self, max_solves):
+        """Record HIP events at every kernel boundary of the next `max_solves` solves."""
+        check(self._L.qsp_set_kernel_timing(self._h, int(max_solves)), "qsp_set_kernel_timing")
+
+    KERNELS = ("prologue", "linearize", "qp_step", "epilogue")
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} over the timed solves since the last call."""
+        ms = (C.c_double * 4)()
+        n = (C.c_int32 * 4)()
+        check(self._L.qsp_get_kernel_times(self._h, ms, n), "qsp_get_kernel_times")
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
+
     # ----------------------------------------------------- building blocks
     def _sid(self, shape_id, n):
         return i32(np.broadcast_to(np.asarray(0 if shape_id is None else shape_id, np.int32), (n,)))
