@@ -75,10 +75,11 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads):
     orc = Oracle(SHAPES)
     op = make_opts(N=N, sqp_iters=K)
 
-    def run(sl, xx=None):
+    def run(sl, xx=None, K_run=K):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
-        return orc.controller_solve(op, xx, traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
+        return orc.controller_solve(op if K_run == K else make_opts(N=N, sqp_iters=K_run), xx, traj, 1, warm,
+                                    shape_id=shape_id[sl], nthreads=threads)
 
     probe = min(len(x0), max(2 * threads, 16))
     t0 = time.perf_counter()
@@ -245,17 +246,20 @@ def main():
         d = np.abs(u0[:n] - u0_ref).max(1)
         m = min(n, 512)
         # a lane is 'stable' when the oracle itself stays put (< 1e-9) under three 1e-13 relative
-        # perturbations of x0: the full-step SQP amplifies rounding on the other lanes (DESIGN.md §6)
+        # perturbations of x0: the full-step SQP amplifies rounding on the other lanes (DESIGN.md §2)
         stable = np.ones(m, bool)
         for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
             rp = run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13))
             stable &= np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
+        # ... and converged (the K-1 and K iterates agree: not a limit cycle of the full-step SQP)
+        stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
         result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
                             "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
                             "stable_lanes": int(stable.sum()), "stable_checked": int(m),
                             "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
                             "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
-                                    "< 1e-9 under three 1e-13 relative perturbations of x0 (non-chaotic lane)"}
+                                    "< 1e-9 under three 1e-13 relative perturbations of x0 and between K-1 and K "
+                                    "iterations (converged, non-chaotic lane)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

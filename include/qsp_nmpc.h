@@ -124,6 +124,8 @@ int qsp_set_init(qsp_solver* s, const double* X /* B x (N+1) x 4 */, const doubl
                  const double* PI /* B x N x 4 or NULL */);                              /* 'init_*' */
 int qsp_solve(qsp_solver* s);                                                           /* .solve() */
 int qsp_get_u0(qsp_solver* s, double* u0 /* B x 2 */);                                  /* get('u',0) */
+/* get_x/u/pi return the last solve's trajectories; after qsp_controller_solve they are the
+ * shifted warm start the controller keeps (xtraj/utraj/ptraj, NMPC_controller.m:392-399). */
 int qsp_get_x(qsp_solver* s, double* X);
 int qsp_get_u(qsp_solver* s, double* U);
 int qsp_get_pi(qsp_solver* s, double* PI);

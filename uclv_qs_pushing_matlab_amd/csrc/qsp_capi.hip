@@ -60,6 +60,7 @@ struct qsp_solver {
     int32_t T = 0;
     bool have_traj = false;
     float last_ms = 0.0f;
+    bool last_controller = false;   // get_x/u/pi: controller mode returns the shifted warm start (utraj/xtraj/ptraj)
     std::vector<hipEvent_t> kev;   // kernel-timing pool (qsp_set_kernel_timing)
     int kev_used = 0;
     std::vector<int> kev_solves;   // event offset of each timed solve
@@ -151,6 +152,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.X_out = s->Xo.as<double>();
     a.U_out = s->Uo.as<double>();
     a.PI_out = s->PIo.as<double>();
+    s->last_controller = false;
     a.status = s->status.as<int32_t>();
     a.sqp_iter = s->sqp_iter.as<int32_t>();
     a.qp_iter = s->qp_iter.as<int32_t>();
@@ -481,15 +483,15 @@ int qsp_get_u0(qsp_solver* s, double* u0) {
 }
 int qsp_get_x(qsp_solver* s, double* X) {
     if (!s || !X) return fail(QSP_ERR_ARG, "qsp_get_x: null argument");
-    return d2h(s, X, s->Xo, (size_t)s->o.batch * (s->o.N + 1) * 4 * 8);
+    return d2h(s, X, s->last_controller ? s->X : s->Xo, (size_t)s->o.batch * (s->o.N + 1) * 4 * 8);
 }
 int qsp_get_u(qsp_solver* s, double* U) {
     if (!s || !U) return fail(QSP_ERR_ARG, "qsp_get_u: null argument");
-    return d2h(s, U, s->Uo, (size_t)s->o.batch * s->o.N * 2 * 8);
+    return d2h(s, U, s->last_controller ? s->U : s->Uo, (size_t)s->o.batch * s->o.N * 2 * 8);
 }
 int qsp_get_pi(qsp_solver* s, double* PI) {
     if (!s || !PI) return fail(QSP_ERR_ARG, "qsp_get_pi: null argument");
-    return d2h(s, PI, s->PIo, (size_t)s->o.batch * s->o.N * 4 * 8);
+    return d2h(s, PI, s->last_controller ? s->PI : s->PIo, (size_t)s->o.batch * s->o.N * 4 * 8);
 }
 int qsp_get_cost(qsp_solver* s, double* c) {
     if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_cost: null argument");
@@ -553,6 +555,7 @@ int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_t
     a.X_out = s->X.as<double>();
     a.U_out = s->U.as<double>();
     a.PI_out = s->PI.as<double>();
+    s->last_controller = true;
     return run_timed(s, a);
 }
 
