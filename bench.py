@@ -69,17 +69,17 @@ def flops_per_solve(N, K, qp_iter_total):
     return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
 
 
-def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads):
+def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0):
     """Oracle (port) timed on a bounded sample of the same workload (cold-start controller solves)."""
     from oracle.oracle import Oracle, make_opts
     orc = Oracle(SHAPES)
-    op = make_opts(N=N, sqp_iters=K)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode)
 
     def run(sl, xx=None, K_run=K):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
-        return orc.controller_solve(op if K_run == K else make_opts(N=N, sqp_iters=K_run), xx, traj, 1, warm,
-                                    shape_id=shape_id[sl], nthreads=threads)
+        return orc.controller_solve(op if K_run == K else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode), xx,
+                                    traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
 
     probe = min(len(x0), max(2 * threads, 16))
     t0 = time.perf_counter()
@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--stages-per-lane", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
+                    help="SQP_RTI: fixed-K full steps (the BASELINE metric); SQP: the reference's merit-backtracking "
+                         "SQP with KKT tolerances (sqp_iters = max_iter)")
     ap.add_argument("--seed", type=int, default=20250303 + 3)
     args = ap.parse_args()
 
@@ -131,7 +134,7 @@ def main():
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
-                       device=local_rank)
+                       device=local_rank, nlp_solver_type=args.nlp)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
 
@@ -208,9 +211,12 @@ def main():
         "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": "BASELINE configs[2]: batch=65536 per GPU, N=20, 4 shapes mixed per lane, "
-                               "K=50 SQP-RTI iterations, cold-start NMPC_controller.solve per lane",
+        "config": {"workload": f"BASELINE configs[2]: batch={B} per GPU, N={N}, 4 shapes mixed per lane, "
+                               + (f"K={K} SQP-RTI iterations" if args.nlp == "SQP_RTI" else
+                                  f"merit-backtracking SQP, max_iter={K}, tol 1e-6")
+                               + ", cold-start NMPC_controller.solve per lane",
                    "global_batch": B * world, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
+                   "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout},
                    "parallelism": f"dp{world} (independent lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
@@ -237,7 +243,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         threads = max(1, min(threads, 16))
-        n, dt, r, run = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads)
+        n, dt, r, run = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, 1 if args.nlp == "SQP" else 0)
         result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
                                   "sample": f"{n} lanes of the same workload (oracle/qsp_oracle.c, OpenMP, "
                                             f"{dt:.1f} s)"}
@@ -252,7 +258,10 @@ def main():
             rp = run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13))
             stable &= np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
         # ... and converged (the K-1 and K iterates agree: not a limit cycle of the full-step SQP)
-        stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
+        if args.nlp == "SQP_RTI":
+            stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
+        else:   # merit SQP: the lanes that met the KKT tolerances
+            stable &= r["status"][:m] == 0
         result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
                             "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
                             "stable_lanes": int(stable.sum()), "stable_checked": int(m),

@@ -43,9 +43,11 @@ extern "C" {
 /* per-lane solver status (acados meaning where one exists) */
 #define QSP_STATUS_SUCCESS 0
 #define QSP_STATUS_NAN 1
-#define QSP_STATUS_MAXITER 2
+#define QSP_STATUS_MAXITER 2      /* QSP_NLP_SQP_MERIT: tolerances not met within sqp_iters */
 
 #define QSP_NLP_SQP_RTI_FIXED 0   /* K full Gauss-Newton steps: the BASELINE metric */
+#define QSP_NLP_SQP_MERIT 1       /* acados 'SQP' + 'merit_backtracking' with KKT tolerances
+                                     (NMPC_controller.m:271-276); sqp_iters = max_iter */
 
 typedef struct qsp_solver qsp_solver;
 
@@ -61,6 +63,11 @@ typedef struct {
     int32_t cost_scale_Ts;    /* 1: stage cost scaled by Ts as acados does             */
     double Ts;                /* sample time, T = N * Ts (NMPC_controller.m:89,221)     */
     double mu0, t_min, frac, sigma_min, mu_stop;  /* interior-point parameters         */
+    /* QSP_NLP_SQP_MERIT only: tol_stat/eq/ineq/comp (NMPC_controller.m:275-276) and the
+     * backtracking line search (alpha *= ls_alpha_red while alpha >= ls_alpha_min,
+     * Armijo constant ls_eps on the l1 merit function) */
+    double tol_stat, tol_eq, tol_ineq, tol_comp;
+    double ls_alpha_min, ls_alpha_red, ls_eps;
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */
@@ -92,6 +99,7 @@ typedef struct {
                                 tangential clip, Euler warm-start rollout, shifted X/U/PI out)    */
     int32_t pad_;
     uint8_t* warm_valid;     /* B, controller mode: 0 = cold start (set to 1 on exit); NULL = always cold */
+    const double* PI_in;     /* B x N x 4  'init_pi' (NULL: zeros); read by QSP_NLP_SQP_MERIT only */
 } qsp_device_io;
 
 /* ---------------------------------------------------------------- lifecycle */

@@ -1,0 +1,106 @@
+"""GPU parity of nlp_mode 1 (acados 'SQP' + 'merit_backtracking' with the tolerances of
+NMPC_controller.m:271-276) against the oracle's restatement (oracle/qsp_oracle.c sqp_solve).
+
+Lanes on which the oracle's own answer moves under 1e-13 perturbations of x0 are excluded
+(DESIGN.md §2); on the rest u0, status, sqp_iter and cost must agree."""
+import numpy as np
+import pytest
+
+from conftest import config2_x0, straight_traj
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+def _stable(run, x0, ref, keys=("u0",)):
+    st = np.ones(len(x0), bool)
+    for f in (1e-13, -1e-13, 3e-13):
+        rp = run(x0 * (1 + f))
+        for kname in keys:
+            st &= np.abs(np.asarray(rp[kname] - ref[kname]).reshape(len(x0), -1)).max(1) < 1e-9
+        st &= rp["iters"] == ref["iters"]
+    return st
+
+
+def test_merit_sqp_ocp_level(oracle):
+    """acados-level solve (X = x0 guess, U = 0, PI = 0), max_iter 30 (NMPC_controller.m:275)."""
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, nb, K = 20, 128, 30
+    x0 = config2_x0(nb, 21)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    yref = np.repeat(traj[None, :N], nb, 0)
+    yref_e = yref[:, N - 1, :4].copy()
+    X0 = np.repeat(x0[:, None], N + 1, 1)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=1)
+
+    def run(x):
+        r = oracle.ocp_solve(op, x, yref, yref_e, X=np.repeat(x[:, None], N + 1, 1), shape_id=sid)
+        r["u0"] = r["U"][:, 0]
+        return r
+    ref = run(x0)
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K, nlp_solver_type="SQP")
+    s.set_shapes([make_shape(n) for n in NAMES], shape_id=sid)
+    s.set("constr_x0", x0)
+    s.set("cost_y_ref", yref)
+    s.set("cost_y_ref_e", yref_e)
+    s.set("init_x", X0)
+    s.set("init_u", np.zeros((nb, N, 2)))
+    s.solve()
+    u0, status, it, cost = s.get_u0(), s.get("status"), s.get("sqp_iter"), s.get_cost()
+    PI = s.get("pi")
+    s.close()
+    assert set(np.unique(status)) <= {0, 2}
+    st = _stable(run, x0, ref)
+    assert st.mean() > 0.5, st.mean()
+    # converged lanes must be converged on the GPU too, after the same number of iterations
+    assert np.all(status[st] == ref["status"][st])
+    assert np.all(it[st] == ref["iters"][st])
+    d = np.abs(u0 - ref["u0"]).max(1)
+    # converged lanes (status 0) agree to the BASELINE tolerance; lanes still iterating at
+    # max_iter carry rounding-level differences that the Armijo test may amplify: 95 %
+    conv = st & (status == 0)
+    assert conv.sum() > 0
+    assert d[conv].max() < 1e-6, np.sort(d[conv])[-4:]
+    np.testing.assert_allclose(cost[conv], ref["cost"][conv], rtol=1e-6, atol=1e-12)
+    assert np.mean(d[st] < 1e-6) > 0.95, np.sort(d[st])[-4:]
+    np.testing.assert_allclose(PI[conv], ref["PI"][conv], rtol=1e-5, atol=1e-7)
+
+
+def test_merit_sqp_controller_two_steps(oracle):
+    """NMPC_controller.solve with the reference's own SQP options, a cold then a warm step."""
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, nb, K = 20, 64, 30
+    x0 = config2_x0(nb, 23)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=1)
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K, nlp_solver_type="SQP")
+    s.set_shapes([make_shape(n) for n in NAMES], shape_id=sid)
+    s.set_reference_trajectory(traj)
+    warm = oracle.new_warm(nb, N)
+    u_g = s.controller_solve(x0, 1)
+    r = oracle.controller_solve(op, x0, traj, 1, warm, shape_id=sid)
+
+    def run(x):
+        return oracle.controller_solve(op, x, traj, 1, oracle.new_warm(nb, N), shape_id=sid)
+    st = _stable(run, x0, r)
+    assert st.mean() > 0.5
+    d = np.abs(u_g - r["u0"]).max(1)
+    conv = st & (r["status"] == 0)
+    assert d[conv].max() < 1e-6, np.sort(d[conv])[-4:]
+    assert np.mean(d[st] < 1e-6) > 0.95, np.sort(d[st])[-4:]
+    assert np.all(s.get("status")[st] == r["status"][st])
+    # second (warm) step on lanes whose first step agreed
+    f, _ = oracle.dynamics(x0, r["u0"], sid)
+    x1 = x0 + 0.05 * f
+    u_g2 = s.controller_solve(x1, 2)
+    r2 = oracle.controller_solve(op, x1, traj, 2, warm, shape_id=sid)
+    d2 = np.abs(u_g2 - r2["u0"]).max(1)
+    ok = st & (d < 1e-9)
+    assert np.mean(d2[ok] < 1e-6) > 0.8, np.sort(d2[ok])[-6:]

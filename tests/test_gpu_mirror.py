@@ -42,7 +42,7 @@ def test_controller_mirror_config1_golden(N):
     from uclv_qs_pushing_matlab_amd.trajectory import TrajectoryGenerator
     gold = json.load(open(os.path.join(GOLDEN, "config1_closed_loop.json")))[f"N{N}"]
     plant = _plant()
-    ctrl = NMPCController("nmpc", plant, 0.05, N, batch=1, sqp_iters=5)
+    ctrl = NMPCController("nmpc", plant, 0.05, N, batch=1, nlp_solver_type="SQP_RTI", sqp_iters=5)
     ctrl.create_ocp_solver()
     tg = TrajectoryGenerator(0.05, 0.01)
     tg.set_target(np.zeros(4), np.zeros(5), 0.0, 10.0)

@@ -25,6 +25,8 @@ class Options(C.Structure):
         ("qp_iters", C.c_int32), ("stages_per_lane", C.c_int32), ("device", C.c_int32), ("cost_scale_Ts", C.c_int32),
         ("Ts", C.c_double), ("mu0", C.c_double), ("t_min", C.c_double), ("frac", C.c_double),
         ("sigma_min", C.c_double), ("mu_stop", C.c_double),
+        ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
+        ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
     ]
 
 
@@ -40,7 +42,8 @@ class Shape(C.Structure):
 class DeviceIO(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in
                 ("x0", "yref", "yref_e", "X_in", "U_in", "shape_id", "u0", "X_out", "U_out", "PI_out", "status",
-                 "cost")] + [("controller", C.c_int32), ("pad_", C.c_int32), ("warm_valid", C.c_void_p)]
+                 "cost")] + [("controller", C.c_int32), ("pad_", C.c_int32), ("warm_valid", C.c_void_p),
+                             ("PI_in", C.c_void_p)]
 
 
 _P = C.c_void_p

@@ -19,8 +19,10 @@ from .solver import OcpSolver
 
 
 class NMPCController:
-    def __init__(self, name, plant, sample_time, Hp, batch=1, sqp_iters=50, qp_iters=20, device=0,
-                 stages_per_lane=0):
+    def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=20,
+                 device=0, stages_per_lane=0):
+        # create_ocp_opts (:270-300): 'SQP' with merit backtracking, max_iter 30, tol 1e-6;
+        # nlp_solver_type='SQP_RTI' gives the fixed-K full-step iteration of the BASELINE metric
         self.name = name
         self.plant = plant
         self.sample_time = sample_time
@@ -42,7 +44,8 @@ class NMPCController:
         self.initial_condition = np.zeros((self.batch, 4))
         self.y_ref = None
         self.cost_function_vect = []
-        self._opts = dict(sqp_iters=sqp_iters, qp_iters=qp_iters, device=device, stages_per_lane=stages_per_lane)
+        self._opts = dict(nlp_solver_type=nlp_solver_type, sqp_iters=sqp_iters, qp_iters=qp_iters, device=device,
+                          stages_per_lane=stages_per_lane)
         self.ocp_solver = None
         self._shape_id = np.zeros(self.batch, np.int32)
 

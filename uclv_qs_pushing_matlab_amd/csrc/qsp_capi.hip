@@ -55,7 +55,7 @@ struct qsp_solver {
     int n_shapes = 0;
     DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
     DevBuf warm_valid, traj, index_time;
-    DevBuf wX, wU, wx0, wlin;
+    DevBuf wX, wU, wx0, wlin, wnlp, wdone;
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
@@ -90,6 +90,13 @@ static void fill_params(qsp_solver* s) {
     p.frac = s->o.frac;
     p.sigma_min = s->o.sigma_min;
     p.mu_stop = s->o.mu_stop;
+    p.tol_stat = s->o.tol_stat;
+    p.tol_eq = s->o.tol_eq;
+    p.tol_ineq = s->o.tol_ineq;
+    p.tol_comp = s->o.tol_comp;
+    p.ls_alpha_min = s->o.ls_alpha_min;
+    p.ls_alpha_red = s->o.ls_alpha_red;
+    p.ls_eps = s->o.ls_eps;
 }
 
 static int auto_S(int N) {
@@ -161,6 +168,9 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wU = s->wU.as<double>();
     a.wx0 = s->wx0.as<double>();
     a.wlin = s->wlin.as<double>();
+    a.wnlp = s->wnlp.as<double>();
+    a.wdone = s->wdone.as<int32_t>();
+    a.PI_in = s->PI.as<double>();   // 'init_pi' (solve) / shifted warm start (controller)
     return a;
 }
 
@@ -225,6 +235,11 @@ void qsp_default_options(qsp_options* o) {
     o->frac = 0.995;
     o->sigma_min = 1e-2;
     o->mu_stop = 1e-10;
+    // nlp_mode 1: NMPC_controller.m:275-276 tolerances; acados merit_backtracking defaults
+    o->tol_stat = o->tol_eq = o->tol_ineq = o->tol_comp = 1e-6;
+    o->ls_alpha_min = 0.05;
+    o->ls_alpha_red = 0.7;
+    o->ls_eps = 1e-4;
 }
 
 int qsp_version(void) { return 1; }
@@ -234,10 +249,16 @@ const char* qsp_last_error(void) { return g_err.c_str(); }
 int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (!o || !out) return fail(QSP_ERR_ARG, "qsp_create: null argument");
     if (o->N < 1 || o->batch < 1) return fail(QSP_ERR_ARG, "qsp_create: N and batch must be >= 1");
-    if (o->nlp_mode != QSP_NLP_SQP_RTI_FIXED) return fail(QSP_ERR_ARG, "qsp_create: unsupported nlp_mode");
+    if (o->nlp_mode != QSP_NLP_SQP_RTI_FIXED && o->nlp_mode != QSP_NLP_SQP_MERIT)
+        return fail(QSP_ERR_ARG, "qsp_create: unsupported nlp_mode");
+    if (o->nlp_mode == QSP_NLP_SQP_MERIT &&
+        (o->N + 1 > 64 || o->stages_per_lane > 1 || !(o->ls_alpha_red > 0.0 && o->ls_alpha_red < 1.0) ||
+         !(o->ls_alpha_min > 0.0 && o->ls_alpha_min <= 1.0)))
+        return fail(QSP_ERR_ARG, "qsp_create: nlp_mode 1 needs N+1 <= 64 (one stage per lane), "
+                                 "0 < ls_alpha_red < 1 and 0 < ls_alpha_min <= 1");
     if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
     if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");
-    int S = o->stages_per_lane > 0 ? o->stages_per_lane : auto_S(o->N);
+    int S = o->stages_per_lane > 0 ? o->stages_per_lane : (o->nlp_mode == QSP_NLP_SQP_MERIT ? 1 : auto_S(o->N));
     if (S < 1 || S > 2) return fail(QSP_ERR_ARG, "qsp_create: stages_per_lane must be 1 or 2");
     if (lanes_per_instance(o->N, S) > 64)
         return fail(QSP_ERR_ARG, "qsp_create: N+1 > 64*stages_per_lane (one instance must fit in a wavefront)");
@@ -280,6 +301,10 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wU, B * N * 2 * 8);
     al(s->wx0, B * 4 * 8);
     al(s->wlin, B * (N + 1) * 24 * 8);
+    if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
+        al(s->wnlp, B * (N + 1) * 20 * 8);
+        al(s->wdone, B * 4);
+    }
     if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->warm_valid.p, 0, B, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->X.p, 0, B * (N + 1) * 4 * 8, s->stream);
@@ -300,7 +325,7 @@ int qsp_destroy(qsp_solver* s) {
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
-                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin};
+                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
     for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);
@@ -573,6 +598,7 @@ int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
     a.yref_e = io->yref_e;
     a.X_in = io->X_in;
     a.U_in = io->U_in;
+    a.PI_in = io->PI_in;
     a.shape_id = io->shape_id ? io->shape_id : s->shape_id.as<int32_t>();
     a.u0 = io->u0;
     a.X_out = io->X_out;

@@ -22,6 +22,7 @@ struct SolveArgs {
     const double* X_in;        // B x (N+1) x 4   initial guess / warm start
     const double* U_in;        // B x N x 2
     uint8_t* warm_valid;       // B (controller mode; nullptr: always cold)
+    const double* PI_in;       // B x N x 4   initial dynamics multipliers (nlp_mode 1; nullptr: zeros)
     double* u0;                // B x 2
     double* X_out;             // B x (N+1) x 4
     double* U_out;             // B x N x 2
@@ -35,6 +36,8 @@ struct SolveArgs {
     double* wU;                // B x N x 2
     double* wx0;               // B x 4           x0 after the controller's s pre-wrap
     double* wlin;              // 24 x B(N+1)     stage data (A, B, defect, gradient), SoA
+    double* wnlp;              // 20 x B(N+1)     nlp_mode 1: PI(4), LAM(6), merit weights NU(4), ETA(6), SoA
+    int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
     // QP-level interface only (qsp_qp_solve): when qp_dx != nullptr the QP kernel
     // reports the QP solution instead of updating the iterate
     double* qp_dx;             // B x (N+1) x 4

@@ -48,6 +48,15 @@ __device__ __forceinline__ double group_min(double v, int base, int L) {
     return __shfl(v, base);
 }
 
+__device__ __forceinline__ double group_max(double v, int base, int L) {
+    const int lig = (int)(threadIdx.x & 63) - base;
+    for (int off = 1; off < L; off <<= 1) {
+        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
+        v = (lig + off < L) ? fmax(v, o) : v;
+    }
+    return __shfl(v, base);
+}
+
 // symmetric 4x4 stored as 10 entries: (0,0)(0,1)(0,2)(0,3)(1,1)(1,2)(1,3)(2,2)(2,3)(3,3)
 __device__ __forceinline__ int sidx(int i, int j) {
     if (i > j) { int t = i; i = j; j = t; }
@@ -416,7 +425,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 // damped control step in LDS (F_DU) and the slacks/multipliers in F_T / F_LM.
 // Returns the number of iterations taken by this lane's instance.
 template <int S>
-__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4]) {
+__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - 1.0);
     // initial point
 #pragma unroll
@@ -447,7 +456,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.base, c.L) / m;
-        const bool done = !(mu >= p.mu_stop);
+        const bool done = skip || !(mu >= p.mu_stop);
         if (__ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
         // ---- predictor
@@ -560,6 +569,23 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
 // Workspace (SolveArgs::w*): SQP iterate X/U, wrapped x0, stage data in SoA.
 enum LinField : int { L_A = 0, L_B = 6, L_BB = 14, L_G = 18, L_COUNT = 24 };
 
+// nlp_mode 1 workspace (SoA over (instance, stage), like wlin)
+enum NlpField : int { W_PI = 0, W_LAM = 4, W_NU = 10, W_ETA = 14, W_COUNT = 20 };
+
+// NLP multipliers and merit weights at the start of a solve (oracle sqp_solve: PI from the
+// initial guess, LAM and the weights zero).
+__device__ __forceinline__ void nlp_init(const SolveArgs& A, int i, bool use_pi) {
+    const int N = A.p.N;
+    const size_t tot = (size_t)A.B * (N + 1);
+    for (int k = 0; k <= N; ++k) {
+        const size_t si = (size_t)i * (N + 1) + k;
+        for (int q = 0; q < 4; ++q)
+            A.wnlp[(W_PI + q) * tot + si] = (use_pi && A.PI_in && k < N) ? A.PI_in[((size_t)i * N + k) * 4 + q] : 0.0;
+        for (int q = W_LAM; q < W_COUNT; ++q) A.wnlp[q * tot + si] = 0.0;
+    }
+    A.wdone[i] = 0;
+}
+
 // NMPC_controller.solve prologue (NMPC_controller.m:332-384) or acados-level init copy.
 __global__ void prologue_kernel(SolveArgs A) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -576,11 +602,13 @@ __global__ void prologue_kernel(SolveArgs A) {
         for (int q = 0; q < (N + 1) * 4; ++q) X[q] = A.X_in[(size_t)i * (N + 1) * 4 + q];
         for (int q = 0; q < N * 2; ++q) U[q] = A.U_in[(size_t)i * N * 2 + q];
         for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
+        if (p.nlp_mode == 1) nlp_init(A, i, true);
         return;
     }
     x0[3] = mat_mod(x0[3], sh.b) - sh.b * ((x0[3] < 0.0) ? 1.0 : 0.0);   // :332
     for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
     const bool cold = (A.warm_valid == nullptr || A.warm_valid[i] == 0);
+    if (p.nlp_mode == 1) nlp_init(A, i, !cold);                             // :351-355 (PI = 0 cold)
     for (int k = 0; k < N; ++k) {                                            // :351-355
         U[2 * k] = cold ? p.cp.u_n_lb : A.U_in[((size_t)i * N + k) * 2];
         U[2 * k + 1] = cold ? 0.0 : A.U_in[((size_t)i * N + k) * 2 + 1];
@@ -610,6 +638,7 @@ __global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
     const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= tot) return;
     const int i = (int)(gi / (N + 1)), k = (int)(gi - (size_t)i * (N + 1));
+    if (p.nlp_mode == 1 && A.wdone[i]) return;                              // converged: iterate frozen
     const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
     const double* X = A.wX + (size_t)i * (N + 1) * 4;
     double* out = A.wlin + gi;
@@ -717,6 +746,291 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     }
 }
 
+// Dynamics multipliers of the QP solution, one per stage lane (S = 1): lane k < N
+// returns pi_k (same adjoint recursion as qp_adjoint_store).
+__device__ __forceinline__ void qp_adjoint_lane(const Ctx& c, const SolveParams& p, const Stage<1>& st,
+                                                double piq[4]) {
+    double pi[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) piq[i] = 0.0;
+    for (int j = c.L - 1; j >= 0; --j) {
+        if (c.lig == j) {
+            if (j == c.N) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pi[i] = p.We[i] * st.dxs(0, i) + st.g[0][i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) piq[i] = pi[i];
+                if (j >= 1) {
+                    const double* a = st.a[0];
+                    double np[4];
+                    np[0] = p.tau * p.W[0] * st.dxs(0, 0) + st.g[0][0] + pi[0];
+                    np[1] = p.tau * p.W[1] * st.dxs(0, 1) + st.g[0][1] + pi[1];
+                    np[2] = p.tau * p.W[2] * st.dxs(0, 2) + st.g[0][2] + (a[0] * pi[0] + a[2] * pi[1] + pi[2]);
+                    np[3] = p.tau * p.W[3] * st.dxs(0, 3) + st.g[0][3] +
+                            (a[1] * pi[0] + a[3] * pi[1] + a[4] * pi[2] + a[5] * pi[3]);
+                    np[3] += st.lm(0, 1) - st.lm(0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pi[i] = np[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pi[i] = wave_from_next(pi[i]);
+    }
+}
+
+// l1 merit contribution of stage k (oracle merit_eval): stage cost, nu'|defect|,
+// eta'(bound violation) on (s_k, u_n, u_t); the terminal lane adds the terminal cost.
+__device__ __forceinline__ double merit_stage(const SolveParams& p, int k, const double x[4], const double u[2],
+                                              const double* yr, const double* ye, const double def[4],
+                                              const double nu[4], const double eta[6]) {
+    if (k == p.N) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const double r = x[i] - ye[i]; s += p.We[i] * r * r; }
+        return 0.5 * s;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const double r = x[i] - yr[i]; s += p.W[i] * r * r; }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { const double r = u[i] - yr[4 + i]; s += p.W[4 + i] * r * r; }
+    double ph = 0.5 * p.tau * s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ph += nu[i] * fabs(def[i]);
+    const double v[3] = {x[3], u[0], u[1]};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (j == 0 && k == 0) continue;
+        const double vl = p.lh[j] - v[j], vh = v[j] - p.uh[j];
+        if (vl > 0.0) ph += eta[2 * j] * vl;
+        if (vh > 0.0) ph += eta[2 * j + 1] * vh;
+    }
+    return ph;
+}
+
+// One SQP iteration of nlp_mode 1 (acados 'SQP' + 'merit_backtracking', restated in the
+// oracle's sqp_solve): KKT test of the current iterate against tol_* (converged instances
+// freeze), the QP, merit weights from the QP multipliers, Armijo backtracking on the l1
+// merit function, damped multiplier update.  One stage per lane (S = 1): lane k of a group
+// owns stage k, so every per-stage term is lane-parallel and the sums/maxima over the
+// horizon are group reductions.
+__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_merit_kernel(SolveArgs A, int it) {
+    extern __shared__ double smem[];
+    const SolveParams& p = A.p;
+    Ctx c;
+    c.lane = threadIdx.x & 63;
+    c.N = p.N;
+    c.L = p.N + 1;
+    const int G = 64 / c.L;
+    c.grp = c.lane / c.L;
+    c.lig = c.lane - c.grp * c.L;
+    c.base = c.grp * c.L;
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    c.inst = wave * G + c.grp;
+    c.real = (c.grp < G) && (c.inst < A.B);
+    const int iv = c.real ? c.inst : A.B - 1;
+    const int N = p.N;
+    const int k = c.lig <= N ? c.lig : N;
+    const bool stg = k < N;
+    const int ku = stg ? k : N - 1;
+    const size_t tot = (size_t)A.B * (N + 1);
+    const size_t si = (size_t)iv * (N + 1) + k;
+    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[iv] : 0];
+    Stage<1> st;
+    st.lds = smem + threadIdx.x;
+    double* X = A.wX + (size_t)iv * (N + 1) * 4;
+    double* U = A.wU + (size_t)iv * N * 2;
+    {
+        const double* in = A.wlin + si;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) st.a[0][q] = in[(L_A + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st.B[0][q] = in[(L_B + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st.bb[0][q] = in[(L_BB + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) st.g[0][q] = in[(L_G + q) * tot];
+    }
+    // stage iterate and NLP multipliers are re-read after the QP instead of being held
+    // in registers across it (the IPM needs every VGPR it can get)
+    auto load_xu = [&](double xk[4], double uk[2]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xk[q] = X[4 * k + q];
+        uk[0] = U[2 * ku];
+        uk[1] = U[2 * ku + 1];
+    };
+    const bool was_done = A.wdone[iv] != 0;
+    bool conv;
+    {
+        double xk[4], uk[2], PIk[4], LAMk[6];
+        load_xu(xk, uk);
+        st.v(0, 0) = xk[3];
+        st.v(0, 1) = uk[0];
+        st.v(0, 2) = uk[1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) PIk[q] = A.wnlp[(W_PI + q) * tot + si];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) LAMk[q] = A.wnlp[(W_LAM + q) * tot + si];
+        // ---- KKT residuals of the NLP at the current iterate (max norms over the horizon)
+        double PIp[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) PIp[q] = wave_from_prev(PIk[q]);   // pi_{k-1}
+        double rs = 0.0, re = 0.0, ri = 0.0, rc = 0.0;
+        if (stg) {
+            const double* B = st.B[0];
+            const double* a = st.a[0];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double r = st.g[0][4 + i] +
+                                 (B[i] * PIk[0] + B[2 + i] * PIk[1] + B[4 + i] * PIk[2] + B[6 + i] * PIk[3]) +
+                                 (LAMk[2 * (1 + i) + 1] - LAMk[2 * (1 + i)]);
+                rs = fmax(rs, fabs(r));
+            }
+            if (k >= 1) {
+                const double at[4] = {PIk[0], PIk[1], a[0] * PIk[0] + a[2] * PIk[1] + PIk[2],
+                                      a[1] * PIk[0] + a[3] * PIk[1] + a[4] * PIk[2] + a[5] * PIk[3]};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    double r = st.g[0][i] - PIp[i] + at[i];
+                    if (i == 3) r += LAMk[1] - LAMk[0];
+                    rs = fmax(rs, fabs(r));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) re = fmax(re, fabs(st.bb[0][i]));
+            const double v[3] = {xk[3], uk[0], uk[1]};
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                if (j == 0 && k == 0) continue;
+                const double sl = v[j] - p.lh[j], sh_ = p.uh[j] - v[j];
+                ri = fmax(ri, fmax(-sl, -sh_));
+                rc = fmax(rc, fmax(fabs(LAMk[2 * j] * sl), fabs(LAMk[2 * j + 1] * sh_)));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rs = fmax(rs, fabs(st.g[0][i] - PIp[i]));
+        }
+        rs = group_max(rs, c.base, c.L);
+        re = group_max(re, c.base, c.L);
+        ri = group_max(ri, c.base, c.L);
+        rc = group_max(rc, c.base, c.L);
+        conv = !was_done && rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
+    }
+    const bool skip = was_done || conv || !c.real;
+    if (conv && c.real && c.lig == 0) {
+        A.wdone[iv] = 1;
+        A.sqp_iter[iv] = it;
+    }
+
+    // ---- QP
+    double dx0[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
+    const int nit = qp_ipm<1>(c, p, st, dx0, skip);
+    qp_rollout<1>(c, st, dx0);
+    double piq[4];
+    qp_adjoint_lane(c, p, st, piq);
+
+    // ---- merit weights, merit value and directional derivative at alpha = 0
+    double xk[4], uk[2], PIk[4], LAMk[6], NUk[4], ETAk[6];
+    load_xu(xk, uk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) PIk[q] = A.wnlp[(W_PI + q) * tot + si];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) LAMk[q] = A.wnlp[(W_LAM + q) * tot + si];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) NUk[q] = A.wnlp[(W_NU + q) * tot + si];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) ETAk[q] = A.wnlp[(W_ETA + q) * tot + si];
+    double dxk[4], duk[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dxk[q] = st.dxs(0, q);
+    duk[0] = stg ? st.du(0, 0) : 0.0;
+    duk[1] = stg ? st.du(0, 1) : 0.0;
+    double lamq[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) lamq[q] = stg ? st.lm(0, q) : 0.0;
+    if (stg) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { const double a = fabs(piq[q]), w = 0.5 * (NUk[q] + a); NUk[q] = a > w ? a : w; }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) { const double a = fabs(lamq[q]), w = 0.5 * (ETAk[q] + a); ETAk[q] = a > w ? a : w; }
+    }
+    const double* yr = A.yref + ((size_t)iv * N + ku) * 6;
+    const double* ye = A.yref_e + (size_t)iv * 4;
+    double dph = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dph += st.g[0][i] * dxk[i];
+    if (stg) {
+        dph += st.g[0][4] * duk[0] + st.g[0][5] * duk[1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dph -= NUk[i] * fabs(st.bb[0][i]);
+        const double v[3] = {xk[3], uk[0], uk[1]};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (j == 0 && k == 0) continue;
+            const double lo = p.lh[j] - v[j], hi = p.uh[j] - v[j];
+            if (lo > 0.0) dph -= ETAk[2 * j] * lo;
+            if (hi < 0.0) dph -= ETAk[2 * j + 1] * (-hi);
+        }
+    }
+    const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, st.bb[0], NUk, ETAk), c.base, c.L);
+    const double dphi = group_sum(dph, c.base, c.L);
+
+    // ---- backtracking: alpha <- red * alpha until Armijo holds or alpha would drop below alpha_min
+    double alpha = 1.0;
+    bool fin = skip;
+    while (__ballot(!fin) != 0ull) {
+        double xt[4], ut[2], xnx[4], def[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xt[q] = xk[q] + alpha * dxk[q];
+        ut[0] = uk[0] + alpha * duk[0];
+        ut[1] = uk[1] + alpha * duk[1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xnx[q] = wave_from_next(xt[q]);   // x_{k+1} + alpha dx_{k+1}
+        if (stg) {
+            Lin Lt;
+            rk4<false>(sh, p.Ts, xt, ut, Lt);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) def[q] = Lt.xn[q] - xnx[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) def[q] = 0.0;
+        }
+        const double phi = group_sum(merit_stage(p, k, xt, ut, yr, ye, def, NUk, ETAk), c.base, c.L);
+        if (!fin) {
+            if (phi <= phi0 + p.ls_eps * alpha * dphi) {
+                fin = true;
+            } else {
+                const double an = alpha * p.ls_alpha_red;
+                if (an < p.ls_alpha_min) fin = true;      // accept the last step tried
+                else alpha = an;
+            }
+        }
+    }
+
+    // ---- update of the iterate and the multipliers
+    if (!skip) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[4 * k + q] = xk[q] + alpha * dxk[q];
+        if (stg) {
+            U[2 * k] = uk[0] + alpha * duk[0];
+            U[2 * k + 1] = uk[1] + alpha * duk[1];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) A.wnlp[(W_PI + q) * tot + si] = PIk[q] + alpha * (piq[q] - PIk[q]);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) A.wnlp[(W_LAM + q) * tot + si] = LAMk[q] + alpha * (lamq[q] - LAMk[q]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) A.wnlp[(W_NU + q) * tot + si] = NUk[q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) A.wnlp[(W_ETA + q) * tot + si] = ETAk[q];
+        }
+    }
+    if (c.real && c.lig == 0) A.qp_iter[iv] += nit;
+}
+
 // status, cost, u0 and the (optionally shifted, NMPC_controller.m:397-399) outputs.
 __global__ void epilogue_kernel(SolveArgs A) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -739,8 +1053,14 @@ __global__ void epilogue_kernel(SolveArgs A) {
     for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s += p.We[q] * r * r; bad |= !isfinite(X[4 * N + q]); }
     cost += 0.5 * s;
     A.cost[i] = cost;
-    A.status[i] = bad ? 1 : 0;
-    A.sqp_iter[i] = p.sqp_iters;
+    if (p.nlp_mode == 1) {
+        const bool conv = A.wdone[i] != 0;                     // sqp_iter was written at convergence
+        A.status[i] = bad ? 1 : (conv ? 0 : 2);
+        if (!conv) A.sqp_iter[i] = p.sqp_iters;
+    } else {
+        A.status[i] = bad ? 1 : 0;
+        A.sqp_iter[i] = p.sqp_iters;
+    }
     A.u0[(size_t)i * 2] = U[0];
     A.u0[(size_t)i * 2 + 1] = U[1];
     const int sh = (A.flags & QSP_FLAG_SHIFT) ? 1 : 0;
@@ -753,6 +1073,15 @@ __global__ void epilogue_kernel(SolveArgs A) {
     for (int k = 0; k < N; ++k) {
         const int src = (k + sh < N) ? k + sh : N - 1;
         for (int q = 0; q < 2; ++q) Uo[2 * k + q] = U[2 * src + q];
+    }
+    if (p.nlp_mode == 1) {
+        // dynamics multipliers of the NLP iterate (shifted like X/U in controller mode)
+        const size_t tot = (size_t)A.B * (N + 1);
+        double* Po = A.PI_out + (size_t)i * N * 4;
+        for (int k = 0; k < N; ++k) {
+            const int src = (k + sh < N) ? k + sh : N - 1;
+            for (int q = 0; q < 4; ++q) Po[4 * k + q] = A.wnlp[(W_PI + q) * tot + (size_t)i * (N + 1) + src];
+        }
     }
     if (A.warm_valid && (A.flags & QSP_FLAG_CONTROLLER)) A.warm_valid[i] = 1;
 }
@@ -836,6 +1165,21 @@ static hipError_t launch_qp_any(const SolveArgs& a, int S, int last, hipStream_t
 
 int lanes_per_instance(int N, int S) { return (N + S) / S; }
 
+static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t stream) {
+    const int L = a.p.N + 1;
+    const int G = 64 / L;
+    const int waves = (a.B + G - 1) / G;
+    const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)sqp_merit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_bytes<1>());
+        attr = true;
+    }
+    hipLaunchKernelGGL(sqp_merit_kernel, dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    return hipGetLastError();
+}
+
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev) {
     int ne = 0;
     auto mark = [&]() { return ev ? hipEventRecord(ev[ne++], stream) : hipSuccess; };
@@ -851,7 +1195,8 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
         hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
         e = hipGetLastError();
         if (e == hipSuccess) e = mark();
-        if (e == hipSuccess) e = launch_qp_any(a, S, it + 1 == a.p.sqp_iters, stream);
+        if (e == hipSuccess)
+            e = a.p.nlp_mode == 1 ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it + 1 == a.p.sqp_iters, stream);
         if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;

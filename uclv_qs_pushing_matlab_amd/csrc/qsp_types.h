@@ -29,7 +29,7 @@ struct CtrlParams {
 // everything a solve needs besides per-lane data
 struct SolveParams {
     int32_t N;            // horizon
-    int32_t nlp_mode;     // 0: fixed-K full-step SQP (RTI metric); 1: reserved (merit line search)
+    int32_t nlp_mode;     // 0: fixed-K full-step SQP (RTI metric); 1: SQP + merit backtracking + KKT tolerances
     int32_t sqp_iters;    // K
     int32_t qp_iters;     // max Mehrotra iterations per QP
     double Ts;            // integrator step h = T / N
@@ -38,6 +38,8 @@ struct SolveParams {
     double We[4];         // diag of W_x_e
     double lh[3], uh[3];  // bounds of h = [s; u_n; u_t]
     double mu0, t_min, frac, sigma_min, mu_stop;  // interior-point parameters
+    double tol_stat, tol_eq, tol_ineq, tol_comp;  // nlp_mode 1 termination
+    double ls_alpha_min, ls_alpha_red, ls_eps;    // nlp_mode 1 line search
     CtrlParams cp;
 };
 

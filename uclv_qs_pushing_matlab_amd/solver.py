@@ -17,8 +17,13 @@ from ._lib import check, f64, i32, ptr
 
 
 class OcpSolver:
+    # nlp_solver_type (NMPC_controller.m:271): 'SQP_RTI' = fixed-K full steps (the BASELINE
+    # metric), 'SQP' = merit backtracking + KKT tolerances (the reference's own options)
+    NLP_MODES = {"SQP_RTI": 0, "SQP": 1}
+
     def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
-                 cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10):
+                 cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10,
+                 nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
         L = _lib.lib()
         o = _lib.Options()
         L.qsp_default_options(C.byref(o))
@@ -26,6 +31,11 @@ class OcpSolver:
         o.sqp_iters, o.qp_iters, o.stages_per_lane, o.device = int(sqp_iters), int(qp_iters), int(stages_per_lane), int(device)
         o.cost_scale_Ts = 1 if cost_scale_Ts else 0
         o.mu0, o.t_min, o.frac, o.sigma_min, o.mu_stop = mu0, t_min, frac, sigma_min, mu_stop
+        if nlp_solver_type not in self.NLP_MODES:
+            raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
+        o.nlp_mode = self.NLP_MODES[nlp_solver_type]
+        o.tol_stat = o.tol_eq = o.tol_ineq = o.tol_comp = float(tol)
+        o.ls_alpha_min, o.ls_alpha_red, o.ls_eps = float(ls_alpha_min), float(ls_alpha_red), float(ls_eps)
         h = C.c_void_p()
         check(L.qsp_create(C.byref(o), C.byref(h)), "qsp_create")
         self._L, self._h, self.opts = L, h, o
