@@ -151,6 +151,13 @@ int qsp_set_reference_trajectory(qsp_solver* s, const double* traj /* T x 6 */, 
  * shifted after every call; u0 is available through qsp_get_u0. */
 int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_time);
 int qsp_controller_reset(qsp_solver* s);                                                 /* clear_variables */
+/* Closed-loop simulation on the device (helper.m:195-322, closed_loop_matlab): cold start,
+ * then for t = 0..n_steps-1: x += noise[t] (sim_noise, optional), u = solve(x, index0 + t),
+ * x += Ts * f(x, u) (evalModelVariableShape + Euler, :292-307).  x0: B x 4; index0: B (1-based);
+ * noise: n_steps x B x 4 or NULL; X_traj: B x (n_steps+1) x 4; U_traj: B x n_steps x 2;
+ * status_traj: B x n_steps (found_sol = status == 0) or NULL. */
+int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int32_t n_steps, const double* noise,
+                    double* X_traj, double* U_traj, int32_t* status_traj);
 
 /* ------------------------------------------------ device-resident fast path */
 int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* hip_stream);

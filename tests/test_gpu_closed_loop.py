@@ -1,0 +1,72 @@
+"""GPU: device-resident closed loop (qsp_closed_loop, helper.m:195-322) against the committed
+config-1 golden trace and against the oracle's controller + Euler plant, batched over
+mixed shapes with sim_noise."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, config2_x0, straight_traj
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_closed_loop_config1_golden(N):
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    gold = json.load(open(os.path.join(GOLDEN, "config1_closed_loop.json")))[f"N{N}"]
+    s = OcpSolver(N=N, batch=4, sqp_iters=5)
+    s.set_shapes([make_shape("santal")])
+    s.set_reference_trajectory(straight_traj())
+    r = s.closed_loop(np.zeros(4), 20)
+    s.close()
+    for lane in range(4):      # identical lanes give identical trajectories
+        np.testing.assert_allclose(r["U"][lane], gold["u0"], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(r["X"][lane, -1], gold["x_final"], atol=1e-9)
+    assert np.all(r["status"] == 0)
+
+
+def test_closed_loop_batched_noise(oracle):
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, nb, K, T = 20, 96, 2, 12
+    x0 = config2_x0(nb, 31)
+    sid = np.arange(nb) % 4
+    rng = np.random.default_rng(5)
+    noise = rng.standard_normal((T, nb, 4)) * np.array([1e-5, 1e-5, 1e-3, 1e-4])   # helper.m:243-245
+    traj = straight_traj()
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K)
+    s.set_shapes([make_shape(n) for n in NAMES], shape_id=sid)
+    s.set_reference_trajectory(traj)
+    r = s.closed_loop(x0, T, index0=1, noise=noise)
+    s.close()
+    op = make_opts(N=N, sqp_iters=K)
+
+    def oracle_loop(xs):
+        warm = oracle.new_warm(nb, N)
+        x = xs + noise[0]
+        X, U = [x], []
+        for t in range(T):
+            ro = oracle.controller_solve(op, x, traj, 1 + t, warm, shape_id=sid)
+            f, _ = oracle.dynamics(x, ro["u0"], sid)
+            x = x + 0.05 * f + (noise[t + 1] if t + 1 < T else 0.0)
+            X.append(x)
+            U.append(ro["u0"])
+        return np.stack(X, 1), np.stack(U, 1)
+    Xo, Uo = oracle_loop(x0)
+    # closed-loop stable lanes: the oracle's own trace does not move under 1e-13 perturbations
+    stable = np.ones(nb, bool)
+    for f in (1e-13, -1e-13):
+        _, Up = oracle_loop(x0 * (1 + f))
+        stable &= np.abs(Up - Uo).max(axis=(1, 2)) < 1e-9
+    assert stable.mean() > 0.4, stable.mean()
+    du = np.abs(r["U"] - Uo).max(axis=(1, 2))
+    dx = np.abs(r["X"] - Xo).max(axis=(1, 2))
+    assert du[stable].max() < 1e-6, np.sort(du[stable])[-4:]
+    assert dx[stable].max() < 1e-8, np.sort(dx[stable])[-4:]
+    assert np.all(r["status"] == 0)

@@ -60,3 +60,23 @@ def test_controller_mirror_config1_golden(N):
         x = x + 0.05 * plant.evalModelVariableShape(x[None], u[None])[0]
     np.testing.assert_allclose(x, gold["x_final"], atol=1e-9)
     assert len(ctrl.cost_function_vect) == 20
+
+
+def test_helper_closed_loop_mirror():
+    """helper.closed_loop_matlab over the mirrors reproduces the config-1 golden trace."""
+    from uclv_qs_pushing_matlab_amd.controller import NMPCController
+    from uclv_qs_pushing_matlab_amd.helper import closed_loop_matlab
+    gold = json.load(open(os.path.join(GOLDEN, "config1_closed_loop.json")))["N20"]
+    plant = _plant()
+    ctrl = NMPCController("nmpc", plant, 0.05, 20, batch=2, nlp_solver_type="SQP_RTI", sqp_iters=5)
+    ctrl.create_ocp_solver()
+    ctrl.initial_condition_update(np.zeros(4))
+    y_ref = np.zeros((6, 201))
+    y_ref[0] = 0.01 * np.arange(201) * 0.05
+    ctrl.set_reference_trajectory(y_ref)
+    out = closed_loop_matlab(plant, ctrl, np.zeros(4), 10.0)
+    u_n, u_t, found = out[6], out[7], out[10]
+    assert u_n.shape == (2, 201) and np.all(found)
+    np.testing.assert_allclose(np.stack([u_n[0, :20], u_t[0, :20]], 1), gold["u0"], atol=1e-9)
+    # the slider tracks the 0.01 m/s line
+    assert abs(out[0][0, -1] - 0.01 * 10.0) < 0.02

@@ -79,6 +79,7 @@ _SIGS = {
     "qsp_set_reference_trajectory": [_P, _P, _I],
     "qsp_controller_solve": [_P, _P, _P],
     "qsp_controller_reset": [_P],
+    "qsp_closed_loop": [_P, _P, _P, _I, _P, _P, _P, _P],
     "qsp_solve_device": [_P, C.POINTER(DeviceIO), _P],
     "qsp_synchronize": [_P],
     "qsp_set_kernel_timing": [_P, _I],

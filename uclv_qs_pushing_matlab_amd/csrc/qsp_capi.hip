@@ -202,19 +202,41 @@ static int check_ids(qsp_solver* s, int32_t n, const int32_t* ids) {
     return QSP_OK;
 }
 
-__global__ void stage_yref_kernel(const double* traj, int T, const int32_t* index_time, int B, int N, double* yref,
-                                  double* yref_e) {
+__global__ void stage_yref_kernel(const double* traj, int T, const int32_t* index_time, int offset, int B, int N,
+                                  double* yref, double* yref_e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     // get_y_ref (NMPC_controller.m:307-313): column index_time+k (1-based), clamped to the last
     for (int k = 0; k < N; ++k) {
-        int idx = index_time[i] + k;
+        int idx = index_time[i] + offset + k;
         if (idx > T) idx = T;
         if (idx < 1) idx = 1;
         for (int c = 0; c < 6; ++c) yref[((size_t)i * N + k) * 6 + c] = traj[(size_t)(idx - 1) * 6 + c];
     }
     // terminal reference = last stage reference (:348)
     for (int c = 0; c < 4; ++c) yref_e[(size_t)i * 4 + c] = yref[((size_t)i * N + N - 1) * 6 + c];
+}
+
+// y_ref staging for the controller step at index_time + offset
+static hipError_t launch_controller_step(qsp_solver* s, int offset) {
+    const size_t B = s->o.batch;
+    hipLaunchKernelGGL(stage_yref_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s->stream,
+                       s->traj.as<double>(), s->T, s->index_time.as<int32_t>(), offset, (int)B, s->o.N,
+                       s->yref.as<double>(), s->yref_e.as<double>());
+    return hipGetLastError();
+}
+
+// NMPC_controller.solve arguments: warm buffers updated in place (each instance reads its
+// own stages before writing), shifted outputs
+static SolveArgs controller_args(qsp_solver* s) {
+    SolveArgs a = make_args(s);
+    a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
+    a.warm_valid = s->warm_valid.as<uint8_t>();
+    a.X_out = s->X.as<double>();
+    a.U_out = s->U.as<double>();
+    a.PI_out = s->PI.as<double>();
+    s->last_controller = true;
+    return a;
 }
 
 extern "C" {
@@ -569,19 +591,51 @@ int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_t
     HIPCHK(s->index_time.ensure(B * 4));
     HIPCHK(hipMemcpyAsync(s->x0.p, x0, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
     HIPCHK(hipMemcpyAsync(s->index_time.p, index_time, B * 4, hipMemcpyHostToDevice, s->stream));
-    hipLaunchKernelGGL(stage_yref_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s->stream,
-                       s->traj.as<double>(), s->T, s->index_time.as<int32_t>(), (int)B, s->o.N, s->yref.as<double>(),
-                       s->yref_e.as<double>());
-    HIPCHK(hipGetLastError());
-    SolveArgs a = make_args(s);
-    a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
-    a.warm_valid = s->warm_valid.as<uint8_t>();
-    // warm buffers are updated in place (each instance reads its own stages before writing)
-    a.X_out = s->X.as<double>();
-    a.U_out = s->U.as<double>();
-    a.PI_out = s->PI.as<double>();
-    s->last_controller = true;
-    return run_timed(s, a);
+    HIPCHK(launch_controller_step(s, 0));
+    return run_timed(s, controller_args(s));
+}
+
+int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int32_t n_steps, const double* noise,
+                    double* X_traj, double* U_traj, int32_t* status_traj) {
+    if (!s || !x0 || !index0 || !X_traj || !U_traj || n_steps < 1)
+        return fail(QSP_ERR_ARG, "qsp_closed_loop: bad argument");
+    if (!s->have_traj) return fail(QSP_ERR_STATE, "qsp_closed_loop: no reference trajectory");
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_closed_loop: no shapes set");
+    const size_t B = s->o.batch, T = (size_t)n_steps;
+    HIPCHK(hipSetDevice(s->o.device));
+    DevBuf& dX = s->scratch[9];
+    DevBuf& dU = s->scratch[10];
+    DevBuf& dS = s->scratch[11];
+    DevBuf& dN = s->scratch[3];
+    HIPCHK(dX.ensure(B * (T + 1) * 4 * 8));
+    HIPCHK(dU.ensure(B * T * 2 * 8));
+    HIPCHK(dS.ensure(B * T * 4));
+    if (noise) HIPCHK(dN.ensure(T * B * 4 * 8));
+    HIPCHK(s->index_time.ensure(B * 4));
+    HIPCHK(hipMemcpyAsync(s->x0.p, x0, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->index_time.p, index0, B * 4, hipMemcpyHostToDevice, s->stream));
+    if (noise) HIPCHK(hipMemcpyAsync(dN.p, noise, T * B * 4 * 8, hipMemcpyHostToDevice, s->stream));
+    // initial_condition_update -> clear_variables: the first solve is a cold start (main.m:79)
+    HIPCHK(hipMemsetAsync(s->warm_valid.p, 0, B, s->stream));
+    const double* nz = noise ? dN.as<double>() : nullptr;
+    HIPCHK(launch_closed_loop_init((int)B, s->x0.as<double>(), nz, dX.as<double>(), n_steps, s->stream));
+    HIPCHK(hipEventRecord(s->ev0, s->stream));
+    const SolveArgs a = controller_args(s);
+    for (int32_t t = 0; t < n_steps; ++t) {
+        HIPCHK(launch_controller_step(s, t));                                  // y_ref for index0 + t
+        HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s)));      // NMPC_controller.solve
+        HIPCHK(launch_plant(s->shapes.as<ShapeDev>(), s->shape_id.as<int32_t>(), (int)B, s->o.Ts, s->x0.as<double>(),
+                            s->u0.as<double>(), s->status.as<int32_t>(), t, n_steps,
+                            (nz && t + 1 < n_steps) ? nz + (size_t)(t + 1) * B * 4 : nullptr, dX.as<double>(),
+                            dU.as<double>(), dS.as<int32_t>(), s->stream));
+    }
+    HIPCHK(hipEventRecord(s->ev1, s->stream));
+    HIPCHK(hipMemcpyAsync(X_traj, dX.p, B * (T + 1) * 4 * 8, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipMemcpyAsync(U_traj, dU.p, B * T * 2 * 8, hipMemcpyDeviceToHost, s->stream));
+    if (status_traj) HIPCHK(hipMemcpyAsync(status_traj, dS.p, B * T * 4, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipEventElapsedTime(&s->last_ms, s->ev0, s->ev1));
+    return QSP_OK;
 }
 
 // ------------------------------------------------------ device fast path

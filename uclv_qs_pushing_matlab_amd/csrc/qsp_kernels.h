@@ -51,6 +51,11 @@ int lanes_per_instance(int N, int S);
 // (prologue | linearize, qp_step x sqp_iters | epilogue), for per-kernel timing.
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
+hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
+                                   hipStream_t stream);
+hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
+                        const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
+                        double* Utraj, int32_t* Straj, hipStream_t stream);
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream);
 hipError_t launch_dynamics(const ShapeDev* shapes, const int32_t* sid, int n, const double* x, const double* u,

@@ -1086,6 +1086,56 @@ __global__ void epilogue_kernel(SolveArgs A) {
     if (A.warm_valid && (A.flags & QSP_FLAG_CONTROLLER)) A.warm_valid[i] = 1;
 }
 
+// ------------------------------------------------------- closed-loop plant
+// helper.m:195-322 (closed_loop_matlab): sim_noise perturbation of x(:,i) before the solve,
+// plant x(:,i+1) = x(:,i) + Ts * evalModelVariableShape(x(:,i), u(:,i)) (:292-307), and the
+// trajectory / found_sol (status) logs.  One thread per lane.
+__global__ void closed_loop_init_kernel(int B, double* x, const double* noise0, double* Xtraj, int n_steps) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    for (int c = 0; c < 4; ++c) {
+        const double v = x[(size_t)i * 4 + c] + (noise0 ? noise0[(size_t)i * 4 + c] : 0.0);
+        x[(size_t)i * 4 + c] = v;
+        Xtraj[((size_t)i * (n_steps + 1)) * 4 + c] = v;
+    }
+}
+
+__global__ void plant_kernel(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
+                             const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
+                             double* Utraj, int32_t* Straj) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const ShapeDev& sh = shapes[sid ? sid[i] : 0];
+    double xi[4] = {x[(size_t)i * 4], x[(size_t)i * 4 + 1], x[(size_t)i * 4 + 2], x[(size_t)i * 4 + 3]};
+    const double u[2] = {u0[(size_t)i * 2], u0[(size_t)i * 2 + 1]};
+    DynOut d;
+    dynamics<false>(sh, xi[2], xi[3], u[0], u[1], d);
+    for (int c = 0; c < 4; ++c) {
+        double v = xi[c] + Ts * d.f[c];
+        if (noise_next) v += noise_next[(size_t)i * 4 + c];
+        x[(size_t)i * 4 + c] = v;
+        Xtraj[((size_t)i * (n_steps + 1) + step + 1) * 4 + c] = v;
+    }
+    Utraj[((size_t)i * n_steps + step) * 2] = u[0];
+    Utraj[((size_t)i * n_steps + step) * 2 + 1] = u[1];
+    if (Straj) Straj[(size_t)i * n_steps + step] = status[i];
+}
+
+hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
+                                   hipStream_t stream) {
+    hipLaunchKernelGGL(closed_loop_init_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, B, x, noise0, Xtraj,
+                       n_steps);
+    return hipGetLastError();
+}
+
+hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
+                        const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
+                        double* Utraj, int32_t* Straj, hipStream_t stream) {
+    hipLaunchKernelGGL(plant_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, shapes, sid, B, Ts, x, u0, status,
+                       step, n_steps, noise_next, Xtraj, Utraj, Straj);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------- building-block kernels
 __global__ void spline_kernel(const ShapeDev* shapes, const int32_t* sid, int n, const double* s,
                               double* C, double* D, double* Dd, double* kappa) {

@@ -217,6 +217,20 @@ class OcpSolver:
         check(self._L.qsp_controller_solve(self._h, ptr(x0), ptr(idx)), "qsp_controller_solve")
         return self.get_u0()
 
+    def closed_loop(self, x0, n_steps, index0=1, noise=None):
+        """Device-resident closed loop (helper.m:195-322): returns X (B, n+1, 4), U (B, n, 2),
+        status (B, n).  noise: (n, B, 4) additive state noise before each solve, or None."""
+        n = int(n_steps)
+        x0 = f64(self._lanes(x0, 4))
+        idx = i32(np.broadcast_to(np.asarray(index0, np.int32), (self.B,)))
+        nz = None if noise is None else f64(noise, (n, self.B, 4))
+        X = np.zeros((self.B, n + 1, 4))
+        U = np.zeros((self.B, n, 2))
+        st = np.zeros((self.B, n), np.int32)
+        check(self._L.qsp_closed_loop(self._h, ptr(x0), ptr(idx), n, ptr(nz), ptr(X), ptr(U), ptr(st)),
+              "qsp_closed_loop")
+        return dict(X=X, U=U, status=st)
+
     def controller_reset(self):
         check(self._L.qsp_controller_reset(self._h), "qsp_controller_reset")
 
