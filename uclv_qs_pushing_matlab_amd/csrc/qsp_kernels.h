@@ -38,6 +38,8 @@ struct SolveArgs {
     double* wlin;              // 24 x B(N+1)     stage data (A, B, defect, gradient), SoA
     double* wnlp;              // 20 x B(N+1)     nlp_mode 1: PI(4), LAM(6), merit weights NU(4), ETA(6), SoA
     int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
+    int32_t* wperm;            // B               wave packing order of the QP kernel (nullptr: identity)
+    int32_t* wnit;             // B               IPM iterations of each instance's last QP
     // QP-level interface only (qsp_qp_solve): when qp_dx != nullptr the QP kernel
     // reports the QP solution instead of updating the iterate
     double* qp_dx;             // B x (N+1) x 4

@@ -684,7 +684,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
     c.real = (c.grp < G) && (c.inst < A.B);
-    const int iv = c.real ? c.inst : A.B - 1;
+    // instances are packed into waves in the order of their previous IPM iteration count
+    // (sort_by_iters_kernel), so the instances sharing a wave finish together
+    const int slot = c.real ? c.inst : A.B - 1;
+    const int iv = A.wperm ? A.wperm[slot] : slot;
     const int N = p.N;
     const size_t tot = (size_t)A.B * (N + 1);
     Stage<S> st;
@@ -742,8 +745,37 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             U[2 * k] += st.du(ls, 0);
             U[2 * k + 1] += st.du(ls, 1);
         }
-        if (k == 0) A.qp_iter[iv] += nit;
+        if (k == 0) {
+            A.qp_iter[iv] += nit;
+            if (A.wnit) A.wnit[iv] = nit;
+        }
     }
+}
+
+// Counting sort of the instances by the IPM iteration count of their last QP (keys
+// 0..qp_iters): one workgroup; the order inside a key is arbitrary and does not affect
+// any result (instances are independent).
+__global__ void __launch_bounds__(1024) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm) {
+    __shared__ int hist[64];
+    __shared__ int off[64];
+    const int tid = threadIdx.x;
+    if (tid < 64) hist[tid] = 0;
+    __syncthreads();
+    // longest first: the waves with the most IPM iterations start first (LPT order), so the
+    // launch does not end on a tail of long waves
+    for (int i = tid; i < B; i += blockDim.x) atomicAdd(&hist[maxkey - min(max(nit[i], 0), maxkey)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int k = 0; k <= maxkey; ++k) { off[k] = acc; acc += hist[k]; }
+    }
+    __syncthreads();
+    for (int i = tid; i < B; i += blockDim.x) perm[atomicAdd(&off[maxkey - min(max(nit[i], 0), maxkey)], 1)] = i;
+}
+
+__global__ void iota_kernel(int B, int32_t* perm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < B) perm[i] = i;
 }
 
 // Dynamics multipliers of the QP solution, one per stage lane (S = 1): lane k < N
@@ -1238,10 +1270,20 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
+    const bool sorted = a.wperm && a.wnit && a.p.nlp_mode == 0 && a.p.qp_iters < 64;
+    if (e == hipSuccess && sorted) {
+        hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = mark();
     const size_t tot = (size_t)a.B * (a.p.N + 1);
     const unsigned gl = (unsigned)((tot + 255) / 256);
     for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
+        if (sorted && it > 0) {
+            hipLaunchKernelGGL(sort_by_iters_kernel, dim3(1), dim3(1024), 0, stream, a.B, a.p.qp_iters, a.wnit, a.wperm);
+            e = hipGetLastError();
+            if (e != hipSuccess) break;
+        }
         hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
         e = hipGetLastError();
         if (e == hipSuccess) e = mark();
