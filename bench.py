@@ -49,12 +49,15 @@ def straight_traj(T_end=10.0, Ts=0.05, v=0.01):
     return traj
 
 
-def make_inputs(B, N, seed):
-    x0 = config2_x0(B, seed)
+def make_inputs(B, N, seed, lo=0, hi=None):
+    """Synthetic config-2/3 inputs for lanes [lo, hi) of a B-lane job (x0 drawn for all B lanes
+    so that every shard sees the same values as a single-process run)."""
+    hi = B if hi is None else hi
+    x0 = config2_x0(B, seed)[lo:hi]
     traj = straight_traj()
-    yref = np.broadcast_to(traj[None, :N], (B, N, 6)).copy()
+    yref = np.broadcast_to(traj[None, :N], (hi - lo, N, 6)).copy()
     yref_e = yref[:, N - 1, :4].copy()
-    shape_id = (np.arange(B) % len(SHAPES)).astype(np.int32)
+    shape_id = (np.arange(lo, hi) % len(SHAPES)).astype(np.int32)
     return x0, yref, yref_e, shape_id, traj
 
 
@@ -129,8 +132,7 @@ def main():
     B, N, K = args.batch, args.N, args.sqp_iters
     # this rank's shard of the global lane set (weak scaling: B lanes per GPU)
     lo, hi = shard_range(B * world, world, rank)
-    x0_all, yref_all, yref_e_all, sid_all, traj = make_inputs(B * world, N, args.seed)
-    x0, yref, yref_e, sid = x0_all[lo:hi], yref_all[lo:hi], yref_e_all[lo:hi], sid_all[lo:hi]
+    x0, yref, yref_e, sid, traj = make_inputs(B * world, N, args.seed, lo, hi)
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,

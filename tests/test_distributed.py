@@ -68,3 +68,12 @@ def test_two_rank_gloo_matches_single_process():
     ref = orc.controller_solve(make_opts(N=10, sqp_iters=2), x0, straight_traj(), 1, orc.new_warm(total, 10),
                                shape_id=np.arange(total) % 4, nthreads=1)
     np.testing.assert_array_equal(u0, ref["u0"])
+
+
+def test_make_inputs_shards_match_single_process():
+    from bench import make_inputs
+    full = make_inputs(1000, 20, 7)
+    for world in (2, 3, 8):
+        parts = [make_inputs(1000, 20, 7, *shard_range(1000, world, r)) for r in range(world)]
+        for q in range(4):
+            np.testing.assert_array_equal(np.concatenate([p[q] for p in parts]), full[q])
