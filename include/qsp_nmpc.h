@@ -147,6 +147,15 @@ int qsp_get_time_tot(qsp_solver* s, double* ms);                                
 /* reference table y_ref (6 x T, MATLAB column-major == T x 6 row-major), shared by all lanes
  * (set_reference_trajectory, NMPC_controller.m:425-431 with delay_buff_comp = 0) */
 int qsp_set_reference_trajectory(qsp_solver* s, const double* traj /* T x 6 */, int32_t T);
+/* one reference table per lane: traj B x T x 6 (scenario sweeps; same staging rule) */
+int qsp_set_reference_trajectories(qsp_solver* s, const double* traj /* B x T x 6 */, int32_t T);
+/* per-lane TrajectoryGenerator.straight_line generated on the device (TrajectoryGenerator.m:39-79):
+ * x0, xf: B x 3 (x, y, theta); samples t0:Ts:tf; rows [x y theta 0 0 0] (main.m:165-178).
+ * Installs the tables as with qsp_set_reference_trajectories; T_out (optional) = samples. */
+int qsp_gen_straight_lines(qsp_solver* s, const double* x0, const double* xf, double t0, double tf,
+                           int32_t auto_angle, int32_t* T_out);
+/* copy of the installed table(s): T x 6 (shared) or B x T x 6 (per lane) */
+int qsp_get_reference_trajectories(qsp_solver* s, double* traj);
 /* x0: B x 4, index_time: B (1-based, as MATLAB).  Warm start lives on the device and is
  * shifted after every call; u0 is available through qsp_get_u0. */
 int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_time);

@@ -77,6 +77,9 @@ _SIGS = {
     "qsp_get_qp_iter": [_P, _P],
     "qsp_get_time_tot": [_P, C.POINTER(_D)],
     "qsp_set_reference_trajectory": [_P, _P, _I],
+    "qsp_set_reference_trajectories": [_P, _P, _I],
+    "qsp_gen_straight_lines": [_P, _P, _P, _D, _D, _I, C.POINTER(_I)],
+    "qsp_get_reference_trajectories": [_P, _P],
     "qsp_controller_solve": [_P, _P, _P],
     "qsp_controller_reset": [_P],
     "qsp_closed_loop": [_P, _P, _P, _I, _P, _P, _P, _P],

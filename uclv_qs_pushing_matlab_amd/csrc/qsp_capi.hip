@@ -59,6 +59,7 @@ struct qsp_solver {
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
+    bool traj_per_lane = false;     // reference table per lane (B x T x 6) instead of shared (T x 6)
     float last_ms = 0.0f;
     bool last_controller = false;   // get_x/u/pi: controller mode returns the shifted warm start (utraj/xtraj/ptraj)
     std::vector<hipEvent_t> kev;   // kernel-timing pool (qsp_set_kernel_timing)
@@ -204,10 +205,11 @@ static int check_ids(qsp_solver* s, int32_t n, const int32_t* ids) {
     return QSP_OK;
 }
 
-__global__ void stage_yref_kernel(const double* traj, int T, const int32_t* index_time, int offset, int B, int N,
-                                  double* yref, double* yref_e) {
+__global__ void stage_yref_kernel(const double* traj, int T, int per_lane, const int32_t* index_time, int offset,
+                                  int B, int N, double* yref, double* yref_e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
+    if (per_lane) traj += (size_t)i * T * 6;
     // get_y_ref (NMPC_controller.m:307-313): column index_time+k (1-based), clamped to the last
     for (int k = 0; k < N; ++k) {
         int idx = index_time[i] + offset + k;
@@ -223,7 +225,8 @@ __global__ void stage_yref_kernel(const double* traj, int T, const int32_t* inde
 static hipError_t launch_controller_step(qsp_solver* s, int offset) {
     const size_t B = s->o.batch;
     hipLaunchKernelGGL(stage_yref_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s->stream,
-                       s->traj.as<double>(), s->T, s->index_time.as<int32_t>(), offset, (int)B, s->o.N,
+                       s->traj.as<double>(), s->T, s->traj_per_lane ? 1 : 0, s->index_time.as<int32_t>(), offset,
+                       (int)B, s->o.N,
                        s->yref.as<double>(), s->yref_e.as<double>());
     return hipGetLastError();
 }
@@ -575,7 +578,52 @@ int qsp_set_reference_trajectory(qsp_solver* s, const double* traj, int32_t T) {
     HIPCHK(hipStreamSynchronize(s->stream));
     s->T = T;
     s->have_traj = true;
+    s->traj_per_lane = false;
     return QSP_OK;
+}
+
+int qsp_set_reference_trajectories(qsp_solver* s, const double* traj, int32_t T) {
+    if (!s || !traj || T < 1) return fail(QSP_ERR_ARG, "qsp_set_reference_trajectories: bad argument");
+    const size_t bytes = (size_t)s->o.batch * T * 6 * 8;
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(s->traj.ensure(bytes));
+    HIPCHK(hipMemcpyAsync(s->traj.p, traj, bytes, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->T = T;
+    s->have_traj = true;
+    s->traj_per_lane = true;
+    return QSP_OK;
+}
+
+int qsp_gen_straight_lines(qsp_solver* s, const double* x0, const double* xf, double t0, double tf,
+                           int32_t auto_angle, int32_t* T_out) {
+    if (!s || !x0 || !xf || !(tf > t0) || t0 < 0.0) return fail(QSP_ERR_ARG, "qsp_gen_straight_lines: bad argument");
+    const size_t B = s->o.batch;
+    // MATLAB t0:Ts:tf
+    const int32_t T = (int32_t)std::floor((tf - t0) / s->o.Ts + 1e-9) + 1;
+    HIPCHK(hipSetDevice(s->o.device));
+    DevBuf& d0 = s->scratch[0];
+    DevBuf& d1 = s->scratch[1];
+    HIPCHK(d0.ensure(B * 3 * 8));
+    HIPCHK(d1.ensure(B * 3 * 8));
+    HIPCHK(hipMemcpyAsync(d0.p, x0, B * 3 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(d1.p, xf, B * 3 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(s->traj.ensure(B * (size_t)T * 6 * 8));
+    HIPCHK(launch_straight_lines((int)B, T, d0.as<double>(), d1.as<double>(), t0, tf, s->o.Ts, auto_angle,
+                                 s->traj.as<double>(), s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->T = T;
+    s->have_traj = true;
+    s->traj_per_lane = true;
+    if (T_out) *T_out = T;
+    return QSP_OK;
+}
+
+int qsp_get_reference_trajectories(qsp_solver* s, double* traj) {
+    if (!s || !traj) return fail(QSP_ERR_ARG, "qsp_get_reference_trajectories: null argument");
+    if (!s->have_traj) return fail(QSP_ERR_STATE, "qsp_get_reference_trajectories: no reference trajectory");
+    const size_t n = (s->traj_per_lane ? (size_t)s->o.batch : 1) * s->T * 6 * 8;
+    return d2h(s, traj, s->traj, n);
 }
 
 int qsp_controller_reset(qsp_solver* s) {

@@ -58,6 +58,8 @@ hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, doubl
 hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
                         const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
                         double* Utraj, int32_t* Straj, hipStream_t stream);
+hipError_t launch_straight_lines(int B, int T, const double* x0, const double* xf, double t0, double tf, double Ts,
+                                 int auto_angle, double* traj, hipStream_t stream);
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream);
 hipError_t launch_dynamics(const ShapeDev* shapes, const int32_t* sid, int n, const double* x, const double* u,

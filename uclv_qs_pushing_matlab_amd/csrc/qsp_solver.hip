@@ -1168,6 +1168,50 @@ hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, doubl
     return hipGetLastError();
 }
 
+// ------------------------------------------------- reference generation
+// TrajectoryGenerator.straight_line (TrajectoryGenerator.m:39-79), one thread per
+// (lane, sample): quintic time scaling s(t) = 6 tau^5 - 15 tau^4 + 10 tau^3, tau = t / tf
+// (:39-42), x(t) = x0 + s(t) (xf - x0) on (x, y, theta); rows [x y theta 0 0 0] as
+// main.m:165-178 builds y_ref (s_ref = 0, u_ref = 0).  auto_angle: theta follows its own
+// quintic over tf / 2 and then holds its final value (:58-66).
+__device__ __forceinline__ double quintic(double t, double tf) {
+    const double tau = t / tf;
+    return ((6.0 * tau - 15.0) * tau + 10.0) * tau * tau * tau;
+}
+
+__global__ void straight_lines_kernel(int B, int T, const double* x0, const double* xf, double t0, double tf,
+                                      double Ts, int auto_angle, double* traj) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (size_t)B * T) return;
+    const int i = (int)(g / T), k = (int)(g - (size_t)i * T);
+    const double t = t0 + k * Ts;
+    const double* a = x0 + (size_t)i * 3;
+    const double* b = xf + (size_t)i * 3;
+    const double s = quintic(t, tf);
+    double* out = traj + g * 6;
+    out[0] = a[0] + s * (b[0] - a[0]);
+    out[1] = a[1] + s * (b[1] - a[1]);
+    if (auto_angle) {
+        const double tfa = 0.5 * tf;
+        const int ka = (int)floor((tfa - t0) / Ts + 1e-9);      // last sample of t0:Ts:tf/2
+        const double ta = t0 + (k < ka ? k : ka) * Ts;
+        out[2] = a[2] + quintic(ta, tf) * (b[2] - a[2]);
+    } else {
+        out[2] = a[2] + s * (b[2] - a[2]);
+    }
+    out[3] = 0.0;
+    out[4] = 0.0;
+    out[5] = 0.0;
+}
+
+hipError_t launch_straight_lines(int B, int T, const double* x0, const double* xf, double t0, double tf, double Ts,
+                                 int auto_angle, double* traj, hipStream_t stream) {
+    const size_t n = (size_t)B * T;
+    hipLaunchKernelGGL(straight_lines_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, B, T, x0, xf,
+                       t0, tf, Ts, auto_angle, traj);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------- building-block kernels
 __global__ void spline_kernel(const ShapeDev* shapes, const int32_t* sid, int n, const double* s,
                               double* C, double* D, double* Dd, double* kappa) {

@@ -210,6 +210,30 @@ class OcpSolver:
         if t.ndim != 2 or t.shape[1] != 6:
             raise ValueError("reference trajectory must be 6 x T")
         check(self._L.qsp_set_reference_trajectory(self._h, ptr(t), t.shape[0]), "qsp_set_reference_trajectory")
+        self._traj_shape = t.shape
+
+    def set_reference_trajectories(self, traj):
+        """Per-lane reference tables: (B, T, 6)."""
+        t = f64(traj)
+        if t.ndim != 3 or t.shape[0] != self.B or t.shape[2] != 6:
+            raise ValueError(f"per-lane references must be (B={self.B}, T, 6), got {t.shape}")
+        check(self._L.qsp_set_reference_trajectories(self._h, ptr(t), t.shape[1]), "qsp_set_reference_trajectories")
+        self._traj_shape = t.shape
+
+    def gen_straight_lines(self, x0, xf, t0, tf, auto_angle=False):
+        """Device-generated TrajectoryGenerator.straight_line per lane (x0, xf: (B, 3)); returns T."""
+        a = f64(self._lanes(x0, 3))
+        b = f64(self._lanes(xf, 3))
+        T = C.c_int32()
+        check(self._L.qsp_gen_straight_lines(self._h, ptr(a), ptr(b), float(t0), float(tf), int(bool(auto_angle)),
+                                             C.byref(T)), "qsp_gen_straight_lines")
+        self._traj_shape = (self.B, T.value, 6)
+        return T.value
+
+    def get_reference_trajectories(self):
+        out = np.zeros(self._traj_shape)
+        check(self._L.qsp_get_reference_trajectories(self._h, ptr(out)), "qsp_get_reference_trajectories")
+        return out
 
     def controller_solve(self, x0, index_time):
         x0 = f64(self._lanes(x0, 4))
