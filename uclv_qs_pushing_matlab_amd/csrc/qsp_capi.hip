@@ -101,9 +101,12 @@ static void fill_params(qsp_solver* s) {
 }
 
 static int auto_S(int N) {
-    // Register-resident layout: one stage per lane is fastest at N = 20 (profiles/ROUND1.md:
-    // 234k vs 224k solves/s for S = 2); two stages per lane once N + 1 exceeds a wavefront.
-    return N + 1 <= 64 ? 1 : 2;
+    // Instances per wavefront G(S) = 64 / ceil((N+1)/S).  One stage per lane keeps the
+    // kernel at 2 waves/SIMD and wins while two stages per lane do not at least double G
+    // (profiles/r01: N = 20 S = 1 239k vs S = 2 224k solves/s; N = 50 S = 2 is 1.32x S = 1).
+    const int g1 = N + 1 <= 64 ? 64 / (N + 1) : 0;
+    const int g2 = 64 / ((N + 2) / 2);
+    return (g1 > 0 && g2 < 2 * g1) ? 1 : 2;
 }
 
 // Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
