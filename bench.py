@@ -78,11 +78,11 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0):
     orc = Oracle(SHAPES)
     op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode)
 
-    def run(sl, xx=None, K_run=K):
+    def run(sl, xx=None, K_run=K, **kw):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
-        return orc.controller_solve(op if K_run == K else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode), xx,
-                                    traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
+        o = op if (K_run == K and not kw) else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode, **kw)
+        return orc.controller_solve(o, xx, traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
 
     probe = min(len(x0), max(2 * threads, 16))
     t0 = time.perf_counter()
@@ -262,6 +262,8 @@ def main():
         # ... and converged (the K-1 and K iterates agree: not a limit cycle of the full-step SQP)
         if args.nlp == "SQP_RTI":
             stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
+            # ... and insensitive to where the IPM stop test (mu < mu_stop) fires
+            stable &= np.abs(run(slice(0, m), mu_stop=1.5e-10)["u0"] - u0_ref[:m]).max(1) < 1e-9
         else:   # merit SQP: the lanes that met the KKT tolerances
             stable &= r["status"][:m] == 0
         result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
@@ -269,8 +271,8 @@ def main():
                             "stable_lanes": int(stable.sum()), "stable_checked": int(m),
                             "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
                             "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
-                                    "< 1e-9 under three 1e-13 relative perturbations of x0 and between K-1 and K "
-                                    "iterations (converged, non-chaotic lane)"}
+                                    "< 1e-9 under three 1e-13 relative perturbations of x0, between K-1 and K "
+                                    "iterations and with mu_stop 1.5e-10 (converged, non-chaotic lane)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

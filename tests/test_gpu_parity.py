@@ -194,12 +194,14 @@ def test_controller_config5_long_horizon(oracle):
     u = s.controller_solve(x0, idx)
     assert np.all(s.get("status") == 0)
     s.close()
-    run = lambda x, k: oracle.controller_solve(make_opts(N=N, sqp_iters=k), x, traj, idx,  # noqa: E731
-                                               oracle.new_warm(nb, N), shape_id=sid)["u0"]
+    run = lambda x, k, **kw: oracle.controller_solve(make_opts(N=N, sqp_iters=k, **kw), x, traj, idx,  # noqa: E731
+                                                     oracle.new_warm(nb, N), shape_id=sid)["u0"]
     ref = run(x0, K)
     stable = np.abs(run(x0, K - 1) - ref).max(1) < 1e-9
-    for f in (1e-13, -1e-13):
+    for f in (1e-13, -1e-13, 3e-13):
         stable &= np.abs(run(x0 * (1 + f), K) - ref).max(1) < 1e-9
+    # one more IPM iteration somewhere (stop test mu < 1e-10 met a rounding later) must not matter
+    stable &= np.abs(run(x0, K, mu_stop=1.5e-10) - ref).max(1) < 1e-9
     assert stable.sum() >= 5, stable.sum()
     d = np.abs(u - ref).max(1)
     assert d[stable].max() < 1e-6, np.sort(d[stable])[-4:]
