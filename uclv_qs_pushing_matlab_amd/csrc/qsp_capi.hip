@@ -55,7 +55,7 @@ struct qsp_solver {
     int n_shapes = 0;
     DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
     DevBuf warm_valid, traj, index_time;
-    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wperm, wnit;
+    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit;
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
@@ -174,6 +174,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wlin = s->wlin.as<double>();
     a.wnlp = s->wnlp.as<double>();
     a.wdone = s->wdone.as<int32_t>();
+    a.wqp = s->wqp.as<double>();
     a.wperm = s->wperm.as<int32_t>();
     a.wnit = s->wnit.as<int32_t>();
     a.PI_in = s->PI.as<double>();   // 'init_pi' (solve) / shifted warm start (controller)
@@ -336,6 +337,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);
         al(s->wdone, B * 4);
+        al(s->wqp, B * (N + 1) * 16 * 8);
     }
     if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->warm_valid.p, 0, B, s->stream);
@@ -357,7 +359,7 @@ int qsp_destroy(qsp_solver* s) {
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
-                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wperm, &s->wnit};
+                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
     for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);

@@ -38,6 +38,7 @@ struct SolveArgs {
     double* wlin;              // 24 x B(N+1)     stage data (A, B, defect, gradient), SoA
     double* wnlp;              // 20 x B(N+1)     nlp_mode 1: PI(4), LAM(6), merit weights NU(4), ETA(6), SoA
     int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
+    double* wqp;               // 16 x B(N+1)     nlp_mode 1: QP step dx(4), du(2), multipliers pi(4), lam(6), SoA
     int32_t* wperm;            // B               wave packing order of the QP kernel (nullptr: identity)
     int32_t* wnit;             // B               IPM iterations of each instance's last QP
     // QP-level interface only (qsp_qp_solve): when qp_dx != nullptr the QP kernel

@@ -669,115 +669,6 @@ __global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
 
 // The QP of one SQP iteration in the register/LDS-resident lane-group layout:
 // load stage data, Mehrotra IPM, roll out the damped step, update the SQP iterate.
-template <int S>
-__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int last) {
-    extern __shared__ double smem[];
-    const SolveParams& p = A.p;
-    Ctx c;
-    c.lane = threadIdx.x & 63;
-    c.N = p.N;
-    c.L = (p.N + S) / S;                 // ceil((N+1)/S)
-    const int G = 64 / c.L;
-    c.grp = c.lane / c.L;
-    c.lig = c.lane - c.grp * c.L;
-    c.base = c.grp * c.L;
-    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    c.inst = wave * G + c.grp;
-    c.real = (c.grp < G) && (c.inst < A.B);
-    // instances are packed into waves in the order of their previous IPM iteration count
-    // (sort_by_iters_kernel), so the instances sharing a wave finish together
-    const int slot = c.real ? c.inst : A.B - 1;
-    const int iv = A.wperm ? A.wperm[slot] : slot;
-    const int N = p.N;
-    const size_t tot = (size_t)A.B * (N + 1);
-    Stage<S> st;
-    st.lds = smem + threadIdx.x;
-    double* X = A.wX + (size_t)iv * (N + 1) * 4;
-    double* U = A.wU + (size_t)iv * N * 2;
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        const int kc = k <= N ? k : N;
-        const int ku = k < N ? k : N - 1;
-        const double* in = A.wlin + (size_t)iv * (N + 1) + kc;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) st.a[ls][q] = in[(L_A + q) * tot];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) st.B[ls][q] = in[(L_B + q) * tot];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) st.bb[ls][q] = in[(L_BB + q) * tot];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) st.g[ls][q] = in[(L_G + q) * tot];
-        st.v(ls, 0) = X[4 * kc + 3];
-        st.v(ls, 1) = U[2 * ku];
-        st.v(ls, 2) = U[2 * ku + 1];
-    }
-    double dx0[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
-    const int nit = qp_ipm<S>(c, p, st, dx0);
-    qp_rollout<S>(c, st, dx0);
-    if (A.qp_dx) {
-        // QP-level interface (qsp_qp_solve): report the QP solution itself
-        if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, false);
-        if (!c.real) return;
-#pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            const int k = kof<S>(c, ls);
-            if (k <= N)
-                for (int q = 0; q < 4; ++q) A.qp_dx[((size_t)iv * (N + 1) + k) * 4 + q] = st.dxs(ls, q);
-            if (k < N) {
-                for (int q = 0; q < 2; ++q) A.qp_du[((size_t)iv * N + k) * 2 + q] = st.du(ls, q);
-                for (int q = 0; q < 6; ++q) A.qp_lam[((size_t)iv * N + k) * 6 + q] = st.lm(ls, q);
-            }
-            if (k == 0) A.qp_iter[iv] = nit;
-        }
-        return;
-    }
-    if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, (A.flags & QSP_FLAG_SHIFT) != 0);
-    if (!c.real) return;
-#pragma unroll
-    for (int ls = 0; ls < S; ++ls) {
-        const int k = kof<S>(c, ls);
-        if (k <= N)
-            for (int q = 0; q < 4; ++q) X[4 * k + q] += st.dxs(ls, q);
-        if (k < N) {
-            U[2 * k] += st.du(ls, 0);
-            U[2 * k + 1] += st.du(ls, 1);
-        }
-        if (k == 0) {
-            A.qp_iter[iv] += nit;
-            if (A.wnit) A.wnit[iv] = nit;
-        }
-    }
-}
-
-// Counting sort of the instances by the IPM iteration count of their last QP (keys
-// 0..qp_iters): one workgroup; the order inside a key is arbitrary and does not affect
-// any result (instances are independent).
-__global__ void __launch_bounds__(1024) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm) {
-    __shared__ int hist[64];
-    __shared__ int off[64];
-    const int tid = threadIdx.x;
-    if (tid < 64) hist[tid] = 0;
-    __syncthreads();
-    // longest first: the waves with the most IPM iterations start first (LPT order), so the
-    // launch does not end on a tail of long waves
-    for (int i = tid; i < B; i += blockDim.x) atomicAdd(&hist[maxkey - min(max(nit[i], 0), maxkey)], 1);
-    __syncthreads();
-    if (tid == 0) {
-        int acc = 0;
-        for (int k = 0; k <= maxkey; ++k) { off[k] = acc; acc += hist[k]; }
-    }
-    __syncthreads();
-    for (int i = tid; i < B; i += blockDim.x) perm[atomicAdd(&off[maxkey - min(max(nit[i], 0), maxkey)], 1)] = i;
-}
-
-__global__ void iota_kernel(int B, int32_t* perm) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < B) perm[i] = i;
-}
-
 // Dynamics multipliers of the QP solution, one per stage lane (S = 1): lane k < N
 // returns pi_k (same adjoint recursion as qp_adjoint_store).
 __device__ __forceinline__ void qp_adjoint_lane(const Ctx& c, const SolveParams& p, const Stage<1>& st,
@@ -842,14 +733,219 @@ __device__ __forceinline__ double merit_stage(const SolveParams& p, int k, const
     return ph;
 }
 
-// One SQP iteration of nlp_mode 1 (acados 'SQP' + 'merit_backtracking', restated in the
-// oracle's sqp_solve): KKT test of the current iterate against tol_* (converged instances
-// freeze), the QP, merit weights from the QP multipliers, Armijo backtracking on the l1
-// merit function, damped multiplier update.  One stage per lane (S = 1): lane k of a group
-// owns stage k, so every per-stage term is lane-parallel and the sums/maxima over the
-// horizon are group reductions.
-__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_merit_kernel(SolveArgs A, int it) {
+// ------------------------------------------------------------------ nlp_mode 1
+// acados 'SQP' + 'merit_backtracking' (NMPC_controller.m:271-276), restated in the
+// oracle's sqp_solve.  One SQP iteration = linearize, qp_step<1, true> (KKT test of the
+// current iterate -> converged instances freeze; QP; its solution into wqp), and
+// merit_ls_kernel (merit weights from the QP multipliers, Armijo backtracking on the l1
+// merit function, damped multiplier update).  One stage per lane: lane k of a group owns
+// stage k, every per-stage term is lane-parallel, horizon sums/maxima are group reductions.
+enum QpField : int { Q_DX = 0, Q_DU = 4, Q_PI = 6, Q_LAM = 10, Q_COUNT = 16 };
+
+// KKT residuals of the NLP at the current iterate against tol_* (max norms over the
+// horizon); `nlp` points at this lane's stage in the W_* SoA (stride tot).
+__device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>& st, const double* nlp, size_t tot) {
+    const int N = p.N;
+    const int k = c.lig;
+    const bool stg = k < N;
+    double PIk[4], LAMk[6];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) PIk[q] = nlp[(W_PI + q) * tot];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) LAMk[q] = nlp[(W_LAM + q) * tot];
+    double PIp[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) PIp[q] = wave_from_prev(PIk[q]);   // pi_{k-1}
+    double rs = 0.0, re = 0.0, ri = 0.0, rc = 0.0;
+    if (stg) {
+        const double* B = st.B[0];
+        const double* a = st.a[0];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double r = st.g[0][4 + i] + (B[i] * PIk[0] + B[2 + i] * PIk[1] + B[4 + i] * PIk[2] + B[6 + i] * PIk[3]) +
+                             (LAMk[2 * (1 + i) + 1] - LAMk[2 * (1 + i)]);
+            rs = fmax(rs, fabs(r));
+        }
+        if (k >= 1) {
+            const double at[4] = {PIk[0], PIk[1], a[0] * PIk[0] + a[2] * PIk[1] + PIk[2],
+                                  a[1] * PIk[0] + a[3] * PIk[1] + a[4] * PIk[2] + a[5] * PIk[3]};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double r = st.g[0][i] - PIp[i] + at[i];
+                if (i == 3) r += LAMk[1] - LAMk[0];
+                rs = fmax(rs, fabs(r));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) re = fmax(re, fabs(st.bb[0][i]));
+        const double v[3] = {st.v(0, 0), st.v(0, 1), st.v(0, 2)};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (j == 0 && k == 0) continue;
+            const double sl = v[j] - p.lh[j], sh_ = p.uh[j] - v[j];
+            ri = fmax(ri, fmax(-sl, -sh_));
+            rc = fmax(rc, fmax(fabs(LAMk[2 * j] * sl), fabs(LAMk[2 * j + 1] * sh_)));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rs = fmax(rs, fabs(st.g[0][i] - PIp[i]));
+    }
+    rs = group_max(rs, c.base, c.L);
+    re = group_max(re, c.base, c.L);
+    ri = group_max(ri, c.base, c.L);
+    rc = group_max(rc, c.base, c.L);
+    return rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
+}
+
+template <int S, bool MERIT = false>
+__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int last) {
     extern __shared__ double smem[];
+    const SolveParams& p = A.p;
+    Ctx c;
+    c.lane = threadIdx.x & 63;
+    c.N = p.N;
+    c.L = (p.N + S) / S;                 // ceil((N+1)/S)
+    const int G = 64 / c.L;
+    c.grp = c.lane / c.L;
+    c.lig = c.lane - c.grp * c.L;
+    c.base = c.grp * c.L;
+    const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    c.inst = wave * G + c.grp;
+    c.real = (c.grp < G) && (c.inst < A.B);
+    // instances are packed into waves in the order of their previous IPM iteration count
+    // (sort_by_iters_kernel), so the instances sharing a wave finish together
+    const int slot = c.real ? c.inst : A.B - 1;
+    const int iv = A.wperm ? A.wperm[slot] : slot;
+    const int N = p.N;
+    const size_t tot = (size_t)A.B * (N + 1);
+    Stage<S> st;
+    st.lds = smem + threadIdx.x;
+    double* X = A.wX + (size_t)iv * (N + 1) * 4;
+    double* U = A.wU + (size_t)iv * N * 2;
+#pragma unroll
+    for (int ls = 0; ls < S; ++ls) {
+        const int k = kof<S>(c, ls);
+        const int kc = k <= N ? k : N;
+        const int ku = k < N ? k : N - 1;
+        const double* in = A.wlin + (size_t)iv * (N + 1) + kc;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) st.a[ls][q] = in[(L_A + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st.B[ls][q] = in[(L_B + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st.bb[ls][q] = in[(L_BB + q) * tot];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) st.g[ls][q] = in[(L_G + q) * tot];
+        st.v(ls, 0) = X[4 * kc + 3];
+        st.v(ls, 1) = U[2 * ku];
+        st.v(ls, 2) = U[2 * ku + 1];
+    }
+    double dx0[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
+    bool skip = false;
+    if constexpr (MERIT) {
+        static_assert(S == 1, "nlp_mode 1 uses one stage per lane");
+        // nlp_mode 1: KKT test of the current iterate; converged instances freeze
+        const bool was_done = A.wdone[iv] != 0;
+        const bool conv = !was_done && nlp_converged(c, p, st, A.wnlp + (size_t)iv * (N + 1) + c.lig, tot);
+        skip = was_done || conv || !c.real;
+        if (conv && c.real && c.lig == 0) {
+            A.wdone[iv] = 1;
+            A.sqp_iter[iv] = last;       // for MERIT, `last` carries the SQP iteration index
+        }
+    }
+    const int nit = qp_ipm<S>(c, p, st, dx0, skip);
+    qp_rollout<S>(c, st, dx0);
+    if constexpr (MERIT) {
+        // QP solution (step, dynamics and bound multipliers) for the line-search kernel
+        double piq[4];
+        qp_adjoint_lane(c, p, st, piq);
+        if (c.real && !skip) {
+            const size_t si = (size_t)iv * (N + 1) + c.lig;
+            double* w = A.wqp + si;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[(Q_DX + q) * tot] = st.dxs(0, q);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) w[(Q_DU + q) * tot] = c.lig < N ? st.du(0, q) : 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[(Q_PI + q) * tot] = piq[q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) w[(Q_LAM + q) * tot] = c.lig < N ? st.lm(0, q) : 0.0;
+        }
+        if (c.real && c.lig == 0) {
+            A.qp_iter[iv] += nit;
+            if (A.wnit) A.wnit[iv] = nit;
+        }
+        return;
+    }
+    if (A.qp_dx) {
+        // QP-level interface (qsp_qp_solve): report the QP solution itself
+        if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, false);
+        if (!c.real) return;
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
+            if (k <= N)
+                for (int q = 0; q < 4; ++q) A.qp_dx[((size_t)iv * (N + 1) + k) * 4 + q] = st.dxs(ls, q);
+            if (k < N) {
+                for (int q = 0; q < 2; ++q) A.qp_du[((size_t)iv * N + k) * 2 + q] = st.du(ls, q);
+                for (int q = 0; q < 6; ++q) A.qp_lam[((size_t)iv * N + k) * 6 + q] = st.lm(ls, q);
+            }
+            if (k == 0) A.qp_iter[iv] = nit;
+        }
+        return;
+    }
+    if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, (A.flags & QSP_FLAG_SHIFT) != 0);
+    if (!c.real) return;
+#pragma unroll
+    for (int ls = 0; ls < S; ++ls) {
+        const int k = kof<S>(c, ls);
+        if (k <= N)
+            for (int q = 0; q < 4; ++q) X[4 * k + q] += st.dxs(ls, q);
+        if (k < N) {
+            U[2 * k] += st.du(ls, 0);
+            U[2 * k + 1] += st.du(ls, 1);
+        }
+        if (k == 0) {
+            A.qp_iter[iv] += nit;
+            if (A.wnit) A.wnit[iv] = nit;
+        }
+    }
+}
+
+// Counting sort of the instances by the IPM iteration count of their last QP (keys
+// 0..qp_iters): one workgroup; the order inside a key is arbitrary and does not affect
+// any result (instances are independent).
+__global__ void __launch_bounds__(1024) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm) {
+    __shared__ int hist[64];
+    __shared__ int off[64];
+    const int tid = threadIdx.x;
+    if (tid < 64) hist[tid] = 0;
+    __syncthreads();
+    // longest first: the waves with the most IPM iterations start first (LPT order), so the
+    // launch does not end on a tail of long waves
+    for (int i = tid; i < B; i += blockDim.x) atomicAdd(&hist[maxkey - min(max(nit[i], 0), maxkey)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int k = 0; k <= maxkey; ++k) { off[k] = acc; acc += hist[k]; }
+    }
+    __syncthreads();
+    for (int i = tid; i < B; i += blockDim.x) perm[atomicAdd(&off[maxkey - min(max(nit[i], 0), maxkey)], 1)] = i;
+}
+
+__global__ void iota_kernel(int B, int32_t* perm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < B) perm[i] = i;
+}
+
+// nlp_mode 1 line search and update (one stage per lane, no LDS): merit weights
+// nu = max(|pi|, (nu + |pi|)/2), eta likewise from the QP bound multipliers; phi(0) and
+// its directional derivative; alpha <- ls_alpha_red * alpha until
+// phi(alpha) <= phi(0) + ls_eps alpha dphi or alpha would drop below ls_alpha_min (then
+// the last alpha tried is taken); X, U, PI, LAM updated with that alpha.
+__global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
     const SolveParams& p = A.p;
     Ctx c;
     c.lane = threadIdx.x & 63;
@@ -869,136 +965,50 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_merit_kernel(SolveAr
     const int ku = stg ? k : N - 1;
     const size_t tot = (size_t)A.B * (N + 1);
     const size_t si = (size_t)iv * (N + 1) + k;
+    // converged instances (this or an earlier iteration) keep their iterate; the QP kernel
+    // wrote no step for them
+    const bool skip = !c.real || A.wdone[iv] != 0;
     const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[iv] : 0];
-    Stage<1> st;
-    st.lds = smem + threadIdx.x;
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
-    {
-        const double* in = A.wlin + si;
+    double xk[4], uk[2], dxk[4], duk[2], piq[4], lamq[6], bb[4], g[6];
+    double PIk[4], LAMk[6], NUk[4], ETAk[6];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) st.a[0][q] = in[(L_A + q) * tot];
+    for (int q = 0; q < 4; ++q) xk[q] = X[4 * k + q];
+    uk[0] = U[2 * ku];
+    uk[1] = U[2 * ku + 1];
+    const double* w = A.wqp + si;
+    const double* in = A.wlin + si;
+    const double* nl = A.wnlp + si;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) st.B[0][q] = in[(L_B + q) * tot];
+    for (int q = 0; q < 4; ++q) { dxk[q] = skip ? 0.0 : w[(Q_DX + q) * tot]; piq[q] = skip ? 0.0 : w[(Q_PI + q) * tot]; }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st.bb[0][q] = in[(L_BB + q) * tot];
+    for (int q = 0; q < 2; ++q) duk[q] = (skip || !stg) ? 0.0 : w[(Q_DU + q) * tot];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) st.g[0][q] = in[(L_G + q) * tot];
-    }
-    // stage iterate and NLP multipliers are re-read after the QP instead of being held
-    // in registers across it (the IPM needs every VGPR it can get)
-    auto load_xu = [&](double xk[4], double uk[2]) {
+    for (int q = 0; q < 6; ++q) lamq[q] = (skip || !stg) ? 0.0 : w[(Q_LAM + q) * tot];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xk[q] = X[4 * k + q];
-        uk[0] = U[2 * ku];
-        uk[1] = U[2 * ku + 1];
-    };
-    const bool was_done = A.wdone[iv] != 0;
-    bool conv;
-    {
-        double xk[4], uk[2], PIk[4], LAMk[6];
-        load_xu(xk, uk);
-        st.v(0, 0) = xk[3];
-        st.v(0, 1) = uk[0];
-        st.v(0, 2) = uk[1];
+    for (int q = 0; q < 4; ++q) bb[q] = in[(L_BB + q) * tot];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) PIk[q] = A.wnlp[(W_PI + q) * tot + si];
+    for (int q = 0; q < 6; ++q) g[q] = in[(L_G + q) * tot];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) LAMk[q] = A.wnlp[(W_LAM + q) * tot + si];
-        // ---- KKT residuals of the NLP at the current iterate (max norms over the horizon)
-        double PIp[4];
+    for (int q = 0; q < 4; ++q) { PIk[q] = nl[(W_PI + q) * tot]; NUk[q] = nl[(W_NU + q) * tot]; }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) PIp[q] = wave_from_prev(PIk[q]);   // pi_{k-1}
-        double rs = 0.0, re = 0.0, ri = 0.0, rc = 0.0;
-        if (stg) {
-            const double* B = st.B[0];
-            const double* a = st.a[0];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const double r = st.g[0][4 + i] +
-                                 (B[i] * PIk[0] + B[2 + i] * PIk[1] + B[4 + i] * PIk[2] + B[6 + i] * PIk[3]) +
-                                 (LAMk[2 * (1 + i) + 1] - LAMk[2 * (1 + i)]);
-                rs = fmax(rs, fabs(r));
-            }
-            if (k >= 1) {
-                const double at[4] = {PIk[0], PIk[1], a[0] * PIk[0] + a[2] * PIk[1] + PIk[2],
-                                      a[1] * PIk[0] + a[3] * PIk[1] + a[4] * PIk[2] + a[5] * PIk[3]};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    double r = st.g[0][i] - PIp[i] + at[i];
-                    if (i == 3) r += LAMk[1] - LAMk[0];
-                    rs = fmax(rs, fabs(r));
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) re = fmax(re, fabs(st.bb[0][i]));
-            const double v[3] = {xk[3], uk[0], uk[1]};
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                if (j == 0 && k == 0) continue;
-                const double sl = v[j] - p.lh[j], sh_ = p.uh[j] - v[j];
-                ri = fmax(ri, fmax(-sl, -sh_));
-                rc = fmax(rc, fmax(fabs(LAMk[2 * j] * sl), fabs(LAMk[2 * j + 1] * sh_)));
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) rs = fmax(rs, fabs(st.g[0][i] - PIp[i]));
-        }
-        rs = group_max(rs, c.base, c.L);
-        re = group_max(re, c.base, c.L);
-        ri = group_max(ri, c.base, c.L);
-        rc = group_max(rc, c.base, c.L);
-        conv = !was_done && rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
-    }
-    const bool skip = was_done || conv || !c.real;
-    if (conv && c.real && c.lig == 0) {
-        A.wdone[iv] = 1;
-        A.sqp_iter[iv] = it;
-    }
-
-    // ---- QP
-    double dx0[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
-    const int nit = qp_ipm<1>(c, p, st, dx0, skip);
-    qp_rollout<1>(c, st, dx0);
-    double piq[4];
-    qp_adjoint_lane(c, p, st, piq);
-
-    // ---- merit weights, merit value and directional derivative at alpha = 0
-    double xk[4], uk[2], PIk[4], LAMk[6], NUk[4], ETAk[6];
-    load_xu(xk, uk);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) PIk[q] = A.wnlp[(W_PI + q) * tot + si];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) LAMk[q] = A.wnlp[(W_LAM + q) * tot + si];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) NUk[q] = A.wnlp[(W_NU + q) * tot + si];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) ETAk[q] = A.wnlp[(W_ETA + q) * tot + si];
-    double dxk[4], duk[2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dxk[q] = st.dxs(0, q);
-    duk[0] = stg ? st.du(0, 0) : 0.0;
-    duk[1] = stg ? st.du(0, 1) : 0.0;
-    double lamq[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) lamq[q] = stg ? st.lm(0, q) : 0.0;
+    for (int q = 0; q < 6; ++q) { LAMk[q] = nl[(W_LAM + q) * tot]; ETAk[q] = nl[(W_ETA + q) * tot]; }
     if (stg) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { const double a = fabs(piq[q]), w = 0.5 * (NUk[q] + a); NUk[q] = a > w ? a : w; }
+        for (int q = 0; q < 4; ++q) { const double a = fabs(piq[q]), wq = 0.5 * (NUk[q] + a); NUk[q] = a > wq ? a : wq; }
 #pragma unroll
-        for (int q = 0; q < 6; ++q) { const double a = fabs(lamq[q]), w = 0.5 * (ETAk[q] + a); ETAk[q] = a > w ? a : w; }
+        for (int q = 0; q < 6; ++q) { const double a = fabs(lamq[q]), wq = 0.5 * (ETAk[q] + a); ETAk[q] = a > wq ? a : wq; }
     }
     const double* yr = A.yref + ((size_t)iv * N + ku) * 6;
     const double* ye = A.yref_e + (size_t)iv * 4;
     double dph = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dph += st.g[0][i] * dxk[i];
+    for (int i = 0; i < 4; ++i) dph += g[i] * dxk[i];
     if (stg) {
-        dph += st.g[0][4] * duk[0] + st.g[0][5] * duk[1];
+        dph += g[4] * duk[0] + g[5] * duk[1];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dph -= NUk[i] * fabs(st.bb[0][i]);
+        for (int i = 0; i < 4; ++i) dph -= NUk[i] * fabs(bb[i]);
         const double v[3] = {xk[3], uk[0], uk[1]};
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -1008,10 +1018,8 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_merit_kernel(SolveAr
             if (hi < 0.0) dph -= ETAk[2 * j + 1] * (-hi);
         }
     }
-    const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, st.bb[0], NUk, ETAk), c.base, c.L);
+    const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, bb, NUk, ETAk), c.base, c.L);
     const double dphi = group_sum(dph, c.base, c.L);
-
-    // ---- backtracking: alpha <- red * alpha until Armijo holds or alpha would drop below alpha_min
     double alpha = 1.0;
     bool fin = skip;
     while (__ballot(!fin) != 0ull) {
@@ -1042,25 +1050,22 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_merit_kernel(SolveAr
             }
         }
     }
-
-    // ---- update of the iterate and the multipliers
-    if (!skip) {
+    if (skip) return;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) X[4 * k + q] = xk[q] + alpha * dxk[q];
-        if (stg) {
-            U[2 * k] = uk[0] + alpha * duk[0];
-            U[2 * k + 1] = uk[1] + alpha * duk[1];
+    for (int q = 0; q < 4; ++q) X[4 * k + q] = xk[q] + alpha * dxk[q];
+    if (stg) {
+        U[2 * k] = uk[0] + alpha * duk[0];
+        U[2 * k + 1] = uk[1] + alpha * duk[1];
+        double* nw = A.wnlp + si;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) A.wnlp[(W_PI + q) * tot + si] = PIk[q] + alpha * (piq[q] - PIk[q]);
+        for (int q = 0; q < 4; ++q) nw[(W_PI + q) * tot] = PIk[q] + alpha * (piq[q] - PIk[q]);
 #pragma unroll
-            for (int q = 0; q < 6; ++q) A.wnlp[(W_LAM + q) * tot + si] = LAMk[q] + alpha * (lamq[q] - LAMk[q]);
+        for (int q = 0; q < 6; ++q) nw[(W_LAM + q) * tot] = LAMk[q] + alpha * (lamq[q] - LAMk[q]);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) A.wnlp[(W_NU + q) * tot + si] = NUk[q];
+        for (int q = 0; q < 4; ++q) nw[(W_NU + q) * tot] = NUk[q];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) A.wnlp[(W_ETA + q) * tot + si] = ETAk[q];
-        }
+        for (int q = 0; q < 6; ++q) nw[(W_ETA + q) * tot] = ETAk[q];
     }
-    if (c.real && c.lig == 0) A.qp_iter[iv] += nit;
 }
 
 // status, cost, u0 and the (optionally shifted, NMPC_controller.m:397-399) outputs.
@@ -1298,11 +1303,14 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)sqp_merit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)qp_step_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   lds_bytes<1>());
         attr = true;
     }
-    hipLaunchKernelGGL(sqp_merit_kernel, dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    hipLaunchKernelGGL((qp_step_kernel<1, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(merit_ls_kernel, dim3((waves * 64 + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -1314,7 +1322,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
-    const bool sorted = a.wperm && a.wnit && a.p.nlp_mode == 0 && a.p.qp_iters < 64;
+    const bool sorted = a.wperm && a.wnit && a.p.qp_iters < 64;
     if (e == hipSuccess && sorted) {
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();
