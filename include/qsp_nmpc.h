@@ -68,6 +68,7 @@ typedef struct {
      * Armijo constant ls_eps on the l1 merit function) */
     double tol_stat, tol_eq, tol_ineq, tol_comp;
     double ls_alpha_min, ls_alpha_red, ls_eps;
+    double res_stop;          /* interior point stops when mu < mu_stop AND the bound residual < res_stop */
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */

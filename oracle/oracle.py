@@ -41,13 +41,14 @@ class Opts(C.Structure):
         ("nlp_mode", C.c_int32), ("pad_", C.c_int32),
         ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
+        ("res_stop", C.c_double),
     ]
 
 
 def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
               W=(1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3), We=(2e5, 2e5, 20.0, 0.0),
               lh=(-0.06, 0.0, -0.05), uh=(0.011, 0.03, 0.05),
-              mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
+              mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
               u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
     o = Opts()
     o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, 0
@@ -59,6 +60,7 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
     o.uh[:] = uh
     o.mu0, o.t_min, o.frac = mu0, t_min, frac
     o.sigma_min, o.mu_stop = sigma_min, mu_stop
+    o.res_stop = res_stop
     o.v_alpha, o.d_v, o.t_angle0 = v_alpha, d_v, t_angle0
     o.u_n_lb, o.u_t_ub = u_n_lb, u_t_ub
     o.nlp_mode = nlp_mode

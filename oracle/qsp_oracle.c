@@ -77,6 +77,7 @@ typedef struct {
     int32_t pad_;
     double tol_stat, tol_eq, tol_ineq, tol_comp;
     double ls_alpha_min, ls_alpha_red, ls_eps;
+    double res_stop;    /* per-QP early exit also needs the bound residual below res_stop */
 } or_opts;
 
 /* ================================================================ dual numbers */
@@ -421,6 +422,10 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     double *dta = dun + 2 * N, *dla = dta + 6 * N;
     double *t = sol->t, *lam = sol->lam;
     int m = 0;
+    /* Bound residual r = v - lo - t (resp. hi - v - t) of the infeasible start: nonzero where
+     * the linearisation point is within t_min of a bound or beyond it.  Every update scales
+     * all residuals by (1 - alpha), so max|r| = r0 * prod(1 - alpha) exactly. */
+    double r0 = 0.0, rscale = 1.0;
     for (int k = 0; k < N; ++k)
         for (int j = 0; j < 3; ++j) {
             for (int sd = 0; sd < 2; ++sd) {
@@ -429,6 +434,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
                     double d = sd == 0 ? -qp->lo[k * 3 + j] : qp->hi[k * 3 + j];
                     t[q] = d > o->t_min ? d : o->t_min;
                     lam[q] = o->mu0 / t[q];
+                    if (t[q] - d > r0) r0 = t[q] - d;
                     m++;
                 } else { t[q] = 1.0; lam[q] = 0.0; }
             }
@@ -441,7 +447,8 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
         mu /= (double)m;
-        if (mu < o->mu_stop) break;
+        /* stop on complementarity AND primal (bound) feasibility (HPIPM checks both) */
+        if (!(mu >= o->mu_stop) && !(r0 * rscale >= o->res_stop)) break;
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
@@ -498,6 +505,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         }
         double alpha = o->frac * amax;
         if (alpha > 1.0) alpha = 1.0;
+        rscale *= 1.0 - alpha;
         for (int q = 0; q < 6 * N; ++q) { t[q] += alpha * dta[q]; lam[q] += alpha * dla[q]; }
         for (int k = 0; k < N; ++k)
             for (int i = 0; i < 2; ++i) sol->du[2 * k + i] += alpha * (dun[2 * k + i] - sol->du[2 * k + i]);

@@ -27,6 +27,7 @@ class Options(C.Structure):
         ("sigma_min", C.c_double), ("mu_stop", C.c_double),
         ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
+        ("res_stop", C.c_double),
     ]
 
 

@@ -91,6 +91,7 @@ static void fill_params(qsp_solver* s) {
     p.frac = s->o.frac;
     p.sigma_min = s->o.sigma_min;
     p.mu_stop = s->o.mu_stop;
+    p.res_stop = s->o.res_stop;
     p.tol_stat = s->o.tol_stat;
     p.tol_eq = s->o.tol_eq;
     p.tol_ineq = s->o.tol_ineq;
@@ -266,6 +267,7 @@ void qsp_default_options(qsp_options* o) {
     o->frac = 0.995;
     o->sigma_min = 1e-2;
     o->mu_stop = 1e-10;
+    o->res_stop = 1e-10;
     // nlp_mode 1: NMPC_controller.m:275-276 tolerances; acados merit_backtracking defaults
     o->tol_stat = o->tol_eq = o->tol_ineq = o->tol_comp = 1e-6;
     o->ls_alpha_min = 0.05;
@@ -334,9 +336,9 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
+    al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);
-        al(s->wdone, B * 4);
         al(s->wqp, B * (N + 1) * 16 * 8);
     }
     if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);

@@ -427,7 +427,9 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 template <int S>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - 1.0);
-    // initial point
+    // initial point.  r0 = largest bound residual of the infeasible start (t - d where the
+    // slack had to be floored at t_min); every update scales all residuals by (1 - alpha)
+    double r0 = 0.0;
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
@@ -437,6 +439,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int j = 0; j < 3; ++j) {
             const bool act = (k < c.N) && (j > 0 || k >= 1);
             const double tl = fmax(-lo[j], p.t_min), th = fmax(hi[j], p.t_min);
+            if (act) r0 = fmax(r0, fmax(tl + lo[j], th - hi[j]));
             const double rl = 1.0 / tl, rh = 1.0 / th;
             st.t(ls, 2 * j) = act ? tl : 1.0;
             st.t(ls, 2 * j + 1) = act ? th : 1.0;
@@ -448,6 +451,8 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         st.du(ls, 0) = 0.0;
         st.du(ls, 1) = 0.0;
     }
+    r0 = group_max(r0, c.base, c.L);
+    double rscale = 1.0;
     int nit = 0;
     for (int it = 0; it < p.qp_iters; ++it) {
         double tl_sum = 0.0;
@@ -456,7 +461,8 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.base, c.L) / m;
-        const bool done = skip || !(mu >= p.mu_stop);
+        // stop on complementarity AND bound feasibility (as HPIPM checks both)
+        const bool done = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop));
         if (__ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
         // ---- predictor
@@ -485,6 +491,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         double alpha = p.frac * group_min(num / den, c.base, c.L);
         alpha = fmin(alpha, 1.0);
         if (done) alpha = 0.0;
+        rscale *= 1.0 - alpha;
         // update (directions are recomputed from the same inputs before t, l change)
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
@@ -598,6 +605,7 @@ __global__ void prologue_kernel(SolveArgs A) {
     double* X = A.wX + (size_t)i * (N + 1) * 4;
     double* U = A.wU + (size_t)i * N * 2;
     A.qp_iter[i] = 0;
+    if (A.wdone) A.wdone[i] = 0;
     if (!(A.flags & QSP_FLAG_CONTROLLER)) {
         for (int q = 0; q < (N + 1) * 4; ++q) X[q] = A.X_in[(size_t)i * (N + 1) * 4 + q];
         for (int q = 0; q < N * 2; ++q) U[q] = A.U_in[(size_t)i * N * 2 + q];
@@ -638,7 +646,7 @@ __global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
     const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gi >= tot) return;
     const int i = (int)(gi / (N + 1)), k = (int)(gi - (size_t)i * (N + 1));
-    if (p.nlp_mode == 1 && A.wdone[i]) return;                              // converged: iterate frozen
+    if (A.wdone && A.wdone[i]) return;                                      // frozen instance
     const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
     const double* X = A.wX + (size_t)i * (N + 1) * 4;
     double* out = A.wlin + gi;
@@ -798,7 +806,7 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
 }
 
 template <int S, bool MERIT = false>
-__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int last) {
+__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
     Ctx c;
@@ -843,25 +851,43 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     double dx0[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
-    bool skip = false;
+    // frozen instances (converged in nlp_mode 1, or a failed QP earlier) are not iterated
+    const bool was_done = A.wdone && A.wdone[iv] != 0;
+    bool skip = was_done;
     if constexpr (MERIT) {
         static_assert(S == 1, "nlp_mode 1 uses one stage per lane");
         // nlp_mode 1: KKT test of the current iterate; converged instances freeze
-        const bool was_done = A.wdone[iv] != 0;
         const bool conv = !was_done && nlp_converged(c, p, st, A.wnlp + (size_t)iv * (N + 1) + c.lig, tot);
         skip = was_done || conv || !c.real;
         if (conv && c.real && c.lig == 0) {
             A.wdone[iv] = 1;
-            A.sqp_iter[iv] = last;       // for MERIT, `last` carries the SQP iteration index
+            A.sqp_iter[iv] = it;
         }
     }
     const int nit = qp_ipm<S>(c, p, st, dx0, skip);
     qp_rollout<S>(c, st, dx0);
+    // a non-finite QP solution stops the instance's SQP with its last iterate (status 1),
+    // as the oracle's sqp_solve does
+    bool failed = false;
+    if (A.wdone) {
+        double bad = 0.0;
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bad = isfinite(st.dxs(ls, q)) ? bad : 1.0;
+            bad = (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1))) ? bad : 1.0;
+        }
+        failed = !skip && group_max(bad, c.base, c.L) > 0.0;
+        if (failed && c.real && c.lig == 0) {
+            A.wdone[iv] = 2;
+            A.sqp_iter[iv] = it;
+        }
+    }
     if constexpr (MERIT) {
         // QP solution (step, dynamics and bound multipliers) for the line-search kernel
         double piq[4];
         qp_adjoint_lane(c, p, st, piq);
-        if (c.real && !skip) {
+        if (c.real && !skip && !failed) {
             const size_t si = (size_t)iv * (N + 1) + c.lig;
             double* w = A.wqp + si;
 #pragma unroll
@@ -879,6 +905,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
         return;
     }
+    const bool last = it + 1 >= p.sqp_iters;
     if (A.qp_dx) {
         // QP-level interface (qsp_qp_solve): report the QP solution itself
         if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, false);
@@ -896,8 +923,11 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
         return;
     }
-    if (last) qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real, (A.flags & QSP_FLAG_SHIFT) != 0);
-    if (!c.real) return;
+    // multipliers of every successful QP (the output holds the last one, also for an
+    // instance that stops early)
+    qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real && !skip && !failed,
+                        (A.flags & QSP_FLAG_SHIFT) != 0);
+    if (!c.real || skip || failed) return;
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
@@ -1090,14 +1120,10 @@ __global__ void epilogue_kernel(SolveArgs A) {
     for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s += p.We[q] * r * r; bad |= !isfinite(X[4 * N + q]); }
     cost += 0.5 * s;
     A.cost[i] = cost;
-    if (p.nlp_mode == 1) {
-        const bool conv = A.wdone[i] != 0;                     // sqp_iter was written at convergence
-        A.status[i] = bad ? 1 : (conv ? 0 : 2);
-        if (!conv) A.sqp_iter[i] = p.sqp_iters;
-    } else {
-        A.status[i] = bad ? 1 : 0;
-        A.sqp_iter[i] = p.sqp_iters;
-    }
+    const int fr = A.wdone ? A.wdone[i] : 0;                   // 1 converged, 2 failed QP (sqp_iter written then)
+    if (p.nlp_mode == 1) A.status[i] = (bad || fr == 2) ? 1 : (fr == 1 ? 0 : 2);
+    else A.status[i] = (bad || fr == 2) ? 1 : 0;
+    if (fr == 0) A.sqp_iter[i] = p.sqp_iters;
     A.u0[(size_t)i * 2] = U[0];
     A.u0[(size_t)i * 2 + 1] = U[1];
     const int sh = (A.flags & QSP_FLAG_SHIFT) ? 1 : 0;
@@ -1271,7 +1297,7 @@ __global__ void vbound_kernel(const ShapeDev* shapes, const int32_t* sid, int n,
 
 // ------------------------------------------------------------------ launchers
 template <int S>
-static hipError_t launch_qp_step(const SolveArgs& a, int last, hipStream_t stream) {
+static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.B + G - 1) / G;
@@ -1282,14 +1308,14 @@ static hipError_t launch_qp_step(const SolveArgs& a, int last, hipStream_t strea
                                   lds_bytes<S>());
         attr = true;
     }
-    hipLaunchKernelGGL(qp_step_kernel<S>, dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, last);
+    hipLaunchKernelGGL(qp_step_kernel<S>, dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
     return hipGetLastError();
 }
 
-static hipError_t launch_qp_any(const SolveArgs& a, int S, int last, hipStream_t stream) {
+static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream) {
     switch (S) {
-        case 1: return launch_qp_step<1>(a, last, stream);
-        case 2: return launch_qp_step<2>(a, last, stream);
+        case 1: return launch_qp_step<1>(a, it, stream);
+        case 2: return launch_qp_step<2>(a, it, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1340,7 +1366,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
         e = hipGetLastError();
         if (e == hipSuccess) e = mark();
         if (e == hipSuccess)
-            e = a.p.nlp_mode == 1 ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it + 1 == a.p.sqp_iters, stream);
+            e = a.p.nlp_mode == 1 ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it, stream);
         if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;
@@ -1351,7 +1377,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
 }
 
 // One QP (qsp_qp_solve): the workspace already holds the stage data.
-hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) { return launch_qp_any(a, S, 1, stream); }
+hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) { return launch_qp_any(a, S, a.p.sqp_iters - 1, stream); }
 
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream) {

@@ -38,6 +38,7 @@ struct SolveParams {
     double We[4];         // diag of W_x_e
     double lh[3], uh[3];  // bounds of h = [s; u_n; u_t]
     double mu0, t_min, frac, sigma_min, mu_stop;  // interior-point parameters
+    double res_stop;                              // IPM stop also needs the bound residual < res_stop
     double tol_stat, tol_eq, tol_ineq, tol_comp;  // nlp_mode 1 termination
     double ls_alpha_min, ls_alpha_red, ls_eps;    // nlp_mode 1 line search
     CtrlParams cp;

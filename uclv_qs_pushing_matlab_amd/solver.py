@@ -22,7 +22,7 @@ class OcpSolver:
     NLP_MODES = {"SQP_RTI": 0, "SQP": 1}
 
     def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
-                 cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10,
+                 cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10,
                  nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
         L = _lib.lib()
         o = _lib.Options()
@@ -31,6 +31,7 @@ class OcpSolver:
         o.sqp_iters, o.qp_iters, o.stages_per_lane, o.device = int(sqp_iters), int(qp_iters), int(stages_per_lane), int(device)
         o.cost_scale_Ts = 1 if cost_scale_Ts else 0
         o.mu0, o.t_min, o.frac, o.sigma_min, o.mu_stop = mu0, t_min, frac, sigma_min, mu_stop
+        o.res_stop = res_stop
         if nlp_solver_type not in self.NLP_MODES:
             raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
         o.nlp_mode = self.NLP_MODES[nlp_solver_type]
