@@ -118,12 +118,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; QSP_DIST_BACKEND=gloo + several ranks per device is only for
+    # rehearsing the multi-rank path on a one-GPU machine
+    backend = os.environ.get("QSP_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    gpu = local_rank % ndev if backend == "gloo" and ndev else local_rank
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the timing reductions
 
     from uclv_qs_pushing_matlab_amd._lib import DeviceIO
     from uclv_qs_pushing_matlab_amd.objects import make_shape
@@ -136,7 +142,7 @@ def main():
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
-                       device=local_rank, nlp_solver_type=args.nlp)
+                       device=gpu, nlp_solver_type=args.nlp)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
 
@@ -184,7 +190,7 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     ktimes = solver.kernel_times()
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # per-lane IPM iteration counts of the (identical) timed solves -> algorithmic flops
@@ -198,7 +204,7 @@ def main():
     qp_avg_s = qp_ms / max(qp_n, 1) * 1e-3
     qp_flops_launch = float(qp_iter.astype(np.float64).sum()) * N * FLOP_IPM_STAGE / K
     if dist:
-        tt = torch.tensor([float(np.count_nonzero(status))], dtype=torch.float64, device=dev)
+        tt = torch.tensor([float(np.count_nonzero(status))], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         nbad = int(tt[0])
     else:
