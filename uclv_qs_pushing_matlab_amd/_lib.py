@@ -106,6 +106,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise QspError(f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    # One HIP runtime per process: the PyTorch wheel bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, linked by its libs under the plain name).  Loading torch first lets
+    # our NEEDED libamdhip64.so.7 bind to that copy; loading ours first would leave torch
+    # initialising a second runtime, which then finds no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     for name, args in _SIGS.items():
         fn = getattr(L, name)

@@ -154,6 +154,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.p = s->p;
     a.B = s->o.batch;
     a.shapes = s->shapes.as<ShapeDev>();
+    a.n_shapes = s->n_shapes;
     a.shape_id = s->shape_id.as<int32_t>();
     a.x0 = s->x0.as<double>();
     a.yref = s->yref.as<double>();

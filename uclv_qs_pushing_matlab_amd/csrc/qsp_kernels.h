@@ -15,7 +15,8 @@ struct SolveArgs {
     int32_t B;
     uint32_t flags;
     const ShapeDev* shapes;
-    const int32_t* shape_id;   // B (nullptr: shape 0)
+    int32_t n_shapes;
+    const int32_t* shape_id;   // B (nullptr: shape 0); clamped into [0, n_shapes)
     const double* x0;          // B x 4
     const double* yref;        // B x N x 6
     const double* yref_e;      // B x 4

@@ -576,6 +576,13 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
 // Workspace (SolveArgs::w*): SQP iterate X/U, wrapped x0, stage data in SoA.
 enum LinField : int { L_A = 0, L_B = 6, L_BB = 14, L_G = 18, L_COUNT = 24 };
 
+// Shape of instance i.  Ids from qsp_solve_device are device data that the host cannot
+// validate without a round trip, so they are clamped into the table here.
+__device__ __forceinline__ const ShapeDev& shape_of(const SolveArgs& A, int i) {
+    const int id = A.shape_id ? A.shape_id[i] : 0;
+    return A.shapes[id < 0 ? 0 : (id >= A.n_shapes ? A.n_shapes - 1 : id)];
+}
+
 // nlp_mode 1 workspace (SoA over (instance, stage), like wlin)
 enum NlpField : int { W_PI = 0, W_LAM = 4, W_NU = 10, W_ETA = 14, W_COUNT = 20 };
 
@@ -599,7 +606,7 @@ __global__ void prologue_kernel(SolveArgs A) {
     if (i >= A.B) return;
     const SolveParams& p = A.p;
     const int N = p.N;
-    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
+    const ShapeDev& sh = shape_of(A, i);
     double x0[4];
     for (int c = 0; c < 4; ++c) x0[c] = A.x0[(size_t)i * 4 + c];
     double* X = A.wX + (size_t)i * (N + 1) * 4;
@@ -647,7 +654,7 @@ __global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
     if (gi >= tot) return;
     const int i = (int)(gi / (N + 1)), k = (int)(gi - (size_t)i * (N + 1));
     if (A.wdone && A.wdone[i]) return;                                      // frozen instance
-    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[i] : 0];
+    const ShapeDev& sh = shape_of(A, i);
     const double* X = A.wX + (size_t)i * (N + 1) * 4;
     double* out = A.wlin + gi;
     if (k < N) {
@@ -998,7 +1005,7 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
     // converged instances (this or an earlier iteration) keep their iterate; the QP kernel
     // wrote no step for them
     const bool skip = !c.real || A.wdone[iv] != 0;
-    const ShapeDev& sh = A.shapes[A.shape_id ? A.shape_id[iv] : 0];
+    const ShapeDev& sh = shape_of(A, iv);
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
     double xk[4], uk[2], dxk[4], duk[2], piq[4], lamq[6], bb[4], g[6];
