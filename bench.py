@@ -248,6 +248,20 @@ def main():
         except Exception:
             pass
 
+    # host-boundary rate (not `value`): NMPC_controller.solve through the C ABI with x0 in
+    # host memory and u0 copied back, y_ref staged on the device from the shared table
+    if world == 1:
+        solver.set_shape_ids(sid)
+        solver.set_reference_trajectory(traj)
+        solver.controller_solve(x0, 1)
+        solver.controller_reset()
+        th = time.perf_counter()
+        nrep = max(1, min(args.steps, 3))
+        for _ in range(nrep):
+            solver.controller_reset()
+            solver.controller_solve(x0, 1)
+        result["host_boundary_solves_per_s"] = Bl * nrep / (time.perf_counter() - th)
+
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         threads = max(1, min(threads, 16))
