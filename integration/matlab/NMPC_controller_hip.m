@@ -29,6 +29,16 @@ classdef NMPC_controller_hip < handle
             self.W_x = W_x; self.W_u = W_u; self.W_x_e = W_x_e;
             qsp_nmpc_mex('cost_W', self.h, [diag(W_x); diag(W_u)], diag(W_x_e));
         end
+        function update_constraints(self, u_n_ub, u_t_ub, u_n_lb, u_t_lb)    % :122-142
+            self.u_n_ub = u_n_ub; self.u_t_ub = u_t_ub; self.u_n_lb = u_n_lb; self.u_t_lb = u_t_lb;
+            qsp_nmpc_mex('constr_h', self.h, [-0.06 u_n_lb u_t_lb], [0.011 u_n_ub u_t_ub]);
+            qsp_nmpc_mex('ctrl_params', self.h, self.v_alpha, self.d_v_bound, self.t_angle0, self.u_n_lb, self.u_t_ub);
+        end
+        function set_delay_comp(self, delay)                                 % :106-110
+            if delay ~= 0
+                error('NMPC_controller_hip:delay', 'only delay = 0 is supported (main.m:74-75)');
+            end
+        end
         function clear_variables(self)                                       % :144-151
             self.y_ref = []; self.cost_function_vect = [];
             qsp_nmpc_mex('reset', self.h);
