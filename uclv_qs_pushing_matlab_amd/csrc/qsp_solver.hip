@@ -3,18 +3,28 @@
 // Lane layout: one NMPC instance owns a group of L = ceil((N+1)/S)
 // consecutive lanes of a wavefront; lane `lig` of the group owns the S horizon
 // stages k = lig*S .. lig*S+S-1 (stage N is the terminal stage).  Every per-stage
-// quantity (iterate, RK4 linearisation, IPM slacks/multipliers, Riccati factors)
-// lives in that lane's VGPRs for the whole solve; nothing spills to HBM between
-// SQP or IPM iterations.  Stage-parallel work (RK4 + sensitivities, barrier terms,
-// step lengths) runs on all lanes at once; the two horizon recursions (Riccati
-// backward, state forward) walk the group lane by lane, handing the 4x4 value
-// function / state step to the neighbour lane with one DPP/bpermute shuffle.
+// quantity (stage model, IPM slacks/multipliers, Riccati factors) lives in that
+// lane's VGPRs or its LDS column for the whole QP; nothing spills to HBM between
+// IPM iterations.  Stage-parallel work (barrier terms, step lengths) runs on all
+// lanes at once; the horizon recursions (Riccati backward, state forward, adjoint)
+// walk the group lane by lane, handing the 4x4 value function / state step to the
+// neighbour lane with one DPP wave shift.
+//
+// One solve = prologue (NMPC_controller.solve wrapper) + K x (linearize [RK4 +
+// sensitivities, one thread per stage], qp_step [one QP per instance]) + epilogue.
+// Before each QP launch the instances are packed into waves by the IPM iteration
+// count of their previous QP, longest first (sort_by_iters_kernel).
 //
 // Algorithm (restating the reference OCP, NMPC_controller.m:174-300):
-//   SQP  : fixed-K full Gauss-Newton steps (BASELINE "SQP-RTI, K iterations")
+//   SQP  : nlp_mode 0 — fixed-K full Gauss-Newton steps (BASELINE "SQP-RTI, K iterations");
+//          nlp_mode 1 — the reference's 'SQP' + 'merit_backtracking': KKT test with
+//          tol 1e-6, l1-merit Armijo backtracking (qp_step<1, true> + merit_ls_kernel)
 //   QP   : box-constrained LQ-OCP, Mehrotra predictor-corrector interior point,
-//          Riccati factorisation reused by the corrector (stands in for HPIPM)
+//          Riccati factorisation reused by the corrector (stands in for HPIPM);
+//          stops on mu < mu_stop and bound residual < res_stop, or at qp_iters
 //   model: RK4 (1 step, h = Ts) + forward sensitivities of f (qsp_math.hpp)
+// Also here: the device closed loop (plant_kernel, helper.m:195-322), per-lane
+// reference generation (straight_lines_kernel) and the building-block kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
