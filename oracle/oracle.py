@@ -74,8 +74,9 @@ def _p(a):
 
 
 class Oracle:
-    def __init__(self, names=("santal", "balea", "montana", "pulirapid"), max_ctrl=64):
-        self.tab = shape_table(names, max_ctrl)
+    def __init__(self, names=("santal", "balea", "montana", "pulirapid"), max_ctrl=64, tab=None):
+        # tab: optional explicit shape table (n_ctrl, ctrl, knots, params) instead of named PLY objects
+        self.tab = shape_table(names, max_ctrl) if tab is None else tab
         t = self.tab
         self._n = np.ascontiguousarray(t["n_ctrl"], np.int32)
         self._c = np.ascontiguousarray(t["ctrl"], np.float64)

@@ -34,3 +34,20 @@ def straight_traj(T_end=10.0, Ts=0.05, v=0.01):
     traj = np.zeros((len(t), 6))
     traj[:, 0] = v * t
     return traj
+
+
+def decagon_table(max_ctrl=64):
+    """Control polygon of acados_nmpc/test_bspline_class.m:22-25 (unit circle at
+    theta = 0:pi/5:2*pi, 11 points, first = last) with the knot rule of :29-33 /
+    PusherSliderModel.m:113-132; c and mu are placeholders (spline tests only)."""
+    from oracle.shapes_np import knots_for
+    th = np.arange(0.0, 2 * np.pi + 1e-12, np.pi / 5)
+    P = np.stack([np.cos(th), np.sin(th)], 1)
+    S, b = knots_for(P)
+    n = len(P)
+    ctrl = np.zeros((1, max_ctrl, 2))
+    ctrl[0, :n] = P
+    knots = np.zeros((1, max_ctrl + 4))
+    knots[0, :n + 4] = S
+    return dict(n_ctrl=np.array([n], np.int32), ctrl=ctrl, knots=knots, params=np.array([[b, 0.03, 0.2]]),
+                max_ctrl=max_ctrl, names=["decagon"]), P, S, b

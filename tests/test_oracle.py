@@ -219,3 +219,25 @@ def test_vbound_definition(oracle):
     kap = oracle.spline(np.mod(s, load_object("santal")["b"]), 0)[4]
     ref = np.minimum(1.0 / (np.abs(np.abs(kap) - 3.0) + 1e-4), 0.05)
     np.testing.assert_allclose(vb, ref, rtol=1e-12)
+
+
+def test_decagon_fixture_known_answers():
+    """test_bspline_class.m's decagon: clamped-end values, end tangent, convex hull,
+    mirror symmetry of the uniform knot vector, C(b) = 0 (half-open indicator)."""
+    from conftest import decagon_table
+    from oracle.oracle import Oracle
+    tab, P, S, b = decagon_table()
+    orc = Oracle(tab=tab)
+    assert len(P) == 11 and len(S) == 15
+    np.testing.assert_allclose(b, 10 * 2 * np.sin(np.pi / 10), rtol=1e-15)
+    C0, _, D0, _, _ = orc.spline(np.array([0.0]), 0)
+    np.testing.assert_allclose(C0[0], P[0], atol=1e-15)                       # clamped start
+    np.testing.assert_allclose(D0[0], 3 * (P[1] - P[0]) / (S[4] - S[1]), rtol=1e-13)
+    s = np.linspace(0, b, 2001)[1:-1]
+    Cs, _, Ds, _, _ = orc.spline(s, 0)
+    assert np.all(np.hypot(Cs[:, 0], Cs[:, 1]) <= 1.0 + 1e-12)                 # convex hull
+    Cm, _, _, _, _ = orc.spline(b - s, 0)
+    np.testing.assert_allclose(Cm[:, 0], Cs[:, 0], atol=1e-13)                 # y -> -y, s -> b - s
+    np.testing.assert_allclose(Cm[:, 1], -Cs[:, 1], atol=1e-13)
+    Cb, _, _, _, _ = orc.spline(np.array([b]), 0)
+    assert np.all(Cb == 0.0)
