@@ -71,3 +71,31 @@ def test_device_shape_ids_are_clamped():
     s.close()
     np.testing.assert_array_equal(u_bad, u_ok)
     assert np.all(status.cpu().numpy() == 0)
+
+
+@pytest.mark.parametrize("mode,S", [("SQP_RTI", 1), ("SQP_RTI", 2), ("SQP", 1)])
+def test_no_uninitialised_reads(monkeypatch, mode, S):
+    """QSP_DEBUG_POISON=1 fills every workspace buffer and the QP kernels' LDS with NaN
+    before use: a kernel that reads a word it never wrote would change the result."""
+    from conftest import config2_x0
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, B = 20, 70
+    x0 = config2_x0(B, 77)
+    sid = np.arange(B) % 4
+
+    def run():
+        s = OcpSolver(N=N, batch=B, sqp_iters=6, stages_per_lane=S, nlp_solver_type=mode)
+        s.set_shapes([make_shape(n) for n in ("santal", "balea", "montana", "pulirapid")], shape_id=sid)
+        s.set_reference_trajectory(straight_traj())
+        u1 = s.controller_solve(x0, 1)
+        u2 = s.controller_solve(x0 * 0.9, 2)          # warm path
+        out = (u1, u2, s.get("status"), s.get("x"), s.get("pi"))
+        s.close()
+        return out
+    clean = run()
+    monkeypatch.setenv("QSP_DEBUG_POISON", "1")
+    poisoned = run()
+    for a, b in zip(clean, poisoned):
+        np.testing.assert_array_equal(a, b)
+    assert np.all(clean[2] == (0 if mode == "SQP_RTI" else clean[2]))

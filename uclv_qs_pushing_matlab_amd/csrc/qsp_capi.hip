@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -61,7 +62,8 @@ struct qsp_solver {
     bool have_traj = false;
     bool traj_per_lane = false;     // reference table per lane (B x T x 6) instead of shared (T x 6)
     float last_ms = 0.0f;
-    bool last_controller = false;   // get_x/u/pi: controller mode returns the shifted warm start (utraj/xtraj/ptraj)
+    bool last_controller = false;
+    bool poison = false;            // QSP_DEBUG_POISON=1: NaN-filled workspace and QP-kernel LDS   // get_x/u/pi: controller mode returns the shifted warm start (utraj/xtraj/ptraj)
     std::vector<hipEvent_t> kev;   // kernel-timing pool (qsp_set_kernel_timing)
     int kev_used = 0;
     std::vector<int> kev_solves;   // event offset of each timed solve
@@ -178,6 +180,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wdone = s->wdone.as<int32_t>();
     a.wqp = s->wqp.as<double>();
     a.wperm = s->wperm.as<int32_t>();
+    if (s->poison) a.flags |= QSP_FLAG_POISON;
     a.wnit = s->wnit.as<int32_t>();
     a.PI_in = s->PI.as<double>();   // 'init_pi' (solve) / shifted warm start (controller)
     return a;
@@ -241,7 +244,7 @@ static hipError_t launch_controller_step(qsp_solver* s, int offset) {
 // own stages before writing), shifted outputs
 static SolveArgs controller_args(qsp_solver* s) {
     SolveArgs a = make_args(s);
-    a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
+    a.flags |= QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
     a.warm_valid = s->warm_valid.as<uint8_t>();
     a.X_out = s->X.as<double>();
     a.U_out = s->U.as<double>();
@@ -347,6 +350,20 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (e == hipSuccess) e = hipMemsetAsync(s->X.p, 0, B * (N + 1) * 4 * 8, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->U.p, 0, B * N * 2 * 8, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->PI.p, 0, B * N * 4 * 8, s->stream);
+    // debug: every workspace byte starts as a NaN pattern, so a kernel that reads a word it
+    // never wrote shows up as NaN (tests/test_gpu_errors.py)
+    const char* pz = std::getenv("QSP_DEBUG_POISON");
+    s->poison = pz && pz[0] == '1';
+    if (s->poison) {
+        DevBuf* ws[] = {&s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
+                        &s->X, &s->U, &s->PI, &s->Xo, &s->Uo, &s->PIo, &s->u0, &s->cost, &s->yref, &s->yref_e};
+        for (DevBuf* b : ws)
+            if (e == hipSuccess && b->p) e = hipMemsetAsync(b->p, 0xff, b->n, s->stream);
+        // ... except what a caller legitimately relies on being zero: the initial guess and warm state
+        if (e == hipSuccess) e = hipMemsetAsync(s->X.p, 0, B * (N + 1) * 4 * 8, s->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(s->U.p, 0, B * N * 2 * 8, s->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(s->PI.p, 0, B * N * 4 * 8, s->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
         std::string m = std::string("qsp_create: ") + hipGetErrorString(e);
@@ -721,7 +738,7 @@ int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
     a.status = io->status;
     a.cost = io->cost;
     if (io->controller) {
-        a.flags = QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
+        a.flags |= QSP_FLAG_CONTROLLER | QSP_FLAG_SHIFT;
         a.warm_valid = io->warm_valid;
     }
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;

@@ -7,6 +7,7 @@
 
 #define QSP_FLAG_CONTROLLER 1u  // NMPC_controller.solve prologue: s pre-wrap, cold/warm start, clip, Euler rollout
 #define QSP_FLAG_SHIFT 2u       // write the warm start shifted by one stage (NMPC_controller.m:397-399)
+#define QSP_FLAG_POISON 4u      // debug (QSP_DEBUG_POISON=1): QP kernels fill their LDS with NaN first
 
 namespace qsp {
 

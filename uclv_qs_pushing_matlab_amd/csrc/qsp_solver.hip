@@ -460,6 +460,13 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         }
         st.du(ls, 0) = 0.0;
         st.du(ls, 1) = 0.0;
+        // the forward walks never write the terminal / padding slots: define them, so no
+        // stale LDS content (another block's data, possibly NaN bit patterns) is ever read
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            st.f(F_VA, ls, q) = 0.0;
+            st.f(F_VN, ls, q) = 0.0;
+        }
     }
     r0 = group_max(r0, c.base, c.L);
     double rscale = 1.0;
@@ -684,6 +691,9 @@ __global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) out[(L_G + 4 + q) * tot] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
     } else {
+        // terminal stage: no dynamics (the QP never reads A, B, b here; defined anyway)
+#pragma unroll
+        for (int q = 0; q < L_G; ++q) out[q * tot] = 0.0;
         const double* ye = A.yref_e + (size_t)i * 4;
 #pragma unroll
         for (int q = 0; q < 4; ++q) out[(L_G + q) * tot] = p.We[q] * (X[4 * N + q] - ye[q]);
@@ -845,6 +855,9 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     const size_t tot = (size_t)A.B * (N + 1);
     Stage<S> st;
     st.lds = smem + threadIdx.x;
+    if (A.flags & QSP_FLAG_POISON) {
+        for (int f = 0; f < F_COUNT * S; ++f) st.lds[f * BLOCK] = __builtin_nan("");
+    }
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
 #pragma unroll
@@ -890,9 +903,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         double bad = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) bad = isfinite(st.dxs(ls, q)) ? bad : 1.0;
-            bad = (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1))) ? bad : 1.0;
+            for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
+            bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
         }
         failed = !skip && group_max(bad, c.base, c.L) > 0.0;
         if (failed && c.real && c.lig == 0) {
