@@ -294,6 +294,8 @@ def main():
                                     "< 1e-9 under three 1e-13 relative perturbations of x0, between K-1 and K "
                                     "iterations and with mu_stop 1.5e-10 (converged, non-chaotic lane)"}
     if rank == 0:
+        if nbad:
+            print(f"bench: WARNING {nbad} of {B * world} lanes returned a non-zero status", file=sys.stderr)
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
