@@ -82,6 +82,21 @@ def main():
         stable &= np.abs(r["u0"] - base["u0"]).max(1) < 1e-9
     np.savez_compressed(os.path.join(HERE, "config2_batch64.npz"), x0=x0, u0=base["u0"], cost=base["cost"],
                         qp_iter=base["qp_iter"], stable=stable)
+
+    # 5. BASELINE configs[0] exactly: santal, N = 20, one SQP-RTI iteration per control step,
+    #    the full 10 s straight-line run (201 steps, helper.m:195-322 with x0 = 0)
+    N, T = 20, 201
+    op = make_opts(N=N, sqp_iters=1)
+    warm = orc.new_warm(1, N)
+    xs = np.zeros((1, 4))
+    U, X = [], [xs[0].copy()]
+    for i in range(1, T + 1):
+        r = orc.controller_solve(op, xs, traj, i, warm)
+        fx, _ = orc.dynamics(xs, r["u0"])
+        xs = xs + 0.05 * fx
+        U.append(r["u0"][0].copy())
+        X.append(xs[0].copy())
+    np.savez_compressed(os.path.join(HERE, "config1_rti_full.npz"), U=np.array(U), X=np.array(X))
     print("golden fixtures written to", HERE, "stable lanes:", int(stable.sum()), "/", nb)
 
 

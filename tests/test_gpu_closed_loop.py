@@ -70,3 +70,19 @@ def test_closed_loop_batched_noise(oracle):
     assert du[stable].max() < 1e-6, np.sort(du[stable])[-4:]
     assert dx[stable].max() < 1e-8, np.sort(dx[stable])[-4:]
     assert np.all(r["status"] == 0)
+
+
+def test_closed_loop_config1_rti_full():
+    """BASELINE configs[0] on the device: 201 steps of one SQP-RTI iteration, one call."""
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    g = np.load(os.path.join(GOLDEN, "config1_rti_full.npz"))
+    s = OcpSolver(N=20, batch=2, sqp_iters=1)
+    s.set_shapes([make_shape("santal")])
+    s.set_reference_trajectory(straight_traj())
+    r = s.closed_loop(np.zeros(4), 201)
+    s.close()
+    for lane in range(2):
+        np.testing.assert_allclose(r["U"][lane], g["U"], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(r["X"][lane], g["X"], rtol=0, atol=1e-8)
+    assert np.all(r["status"] == 0)

@@ -241,3 +241,19 @@ def test_decagon_fixture_known_answers():
     np.testing.assert_allclose(Cm[:, 1], -Cs[:, 1], atol=1e-13)
     Cb, _, _, _, _ = orc.spline(np.array([b]), 0)
     assert np.all(Cb == 0.0)
+
+
+def test_config1_rti_full_golden(oracle):
+    """BASELINE configs[0]: 201 control steps, one SQP-RTI iteration each."""
+    g = np.load(os.path.join(GOLDEN, "config1_rti_full.npz"))
+    op = make_opts(N=20, sqp_iters=1)
+    warm = oracle.new_warm(1, 20)
+    xs = np.zeros((1, 4))
+    traj = straight_traj()
+    for i in range(1, 202):
+        r = oracle.controller_solve(op, xs, traj, i, warm)
+        np.testing.assert_allclose(r["u0"][0], g["U"][i - 1], rtol=0, atol=1e-12)
+        fx, _ = oracle.dynamics(xs, r["u0"])
+        xs = xs + 0.05 * fx
+    np.testing.assert_allclose(xs[0], g["X"][-1], atol=1e-12)
+    assert abs(xs[0, 0] - 0.1) < 2e-3                       # reaches the 0.10 m waypoint
