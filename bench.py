@@ -99,8 +99,8 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536, help="lanes per GPU")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--sqp-iters", type=int, default=50)
