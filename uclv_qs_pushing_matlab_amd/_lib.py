@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libqsp_nmpc.so")
+# QSP_LIB_PATH: developer override (A/B runs of differently compiled libraries)
+LIB_PATH = os.environ.get("QSP_LIB_PATH") or os.path.join(_PKG, "libqsp_nmpc.so")
 MAX_CTRL = 64
 
 _lib = None

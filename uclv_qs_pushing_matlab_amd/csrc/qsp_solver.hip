@@ -67,6 +67,17 @@ __device__ __forceinline__ double group_max(double v, int base, int L) {
     return __shfl(v, base);
 }
 
+// 1/x from the hardware reciprocal refined by two Newton steps (≈ 5 instructions
+// instead of the ≈ 10 of the IEEE division sequence); for the positive, finite
+// arguments it is used on (slacks, a 2x2 determinant) it agrees with 1.0/x to an ulp.
+__device__ __forceinline__ double rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
 // symmetric 4x4 stored as 10 entries: (0,0)(0,1)(0,2)(0,3)(1,1)(1,2)(1,3)(2,2)(2,3)(3,3)
 __device__ __forceinline__ int sidx(int i, int j) {
     if (i > j) { int t = i; i = j; j = t; }
@@ -225,7 +236,7 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     qt[2] = gx[2] + (a[0] * pp[0] + a[2] * pp[1] + pp[2]);
     qt[3] = gx[3] + (a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3]);
     // R~^-1
-    const double idet = 1.0 / (R00 * R11 - R01 * R01);
+    const double idet = rcp(R00 * R11 - R01 * R01);
     Ri[0] = R11 * idet; Ri[1] = -R01 * idet; Ri[2] = R00 * idet;
     // K = -R~^-1 S~ ; kk = -R~^-1 r~
 #pragma unroll
@@ -337,8 +348,8 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
             const double tln = tl + alpha * dtl, thn = th + alpha * dth;
             st.t(ls, 2 * j) = tln;
             st.t(ls, 2 * j + 1) = thn;
-            st.rt(ls, 2 * j) = 1.0 / tln;
-            st.rt(ls, 2 * j + 1) = 1.0 / thn;
+            st.rt(ls, 2 * j) = rcp(tln);
+            st.rt(ls, 2 * j + 1) = rcp(thn);
             st.lm(ls, 2 * j) = ll + alpha * dll;
             st.lm(ls, 2 * j + 1) = lh + alpha * dlh;
         } else {
@@ -450,7 +461,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
             const bool act = (k < c.N) && (j > 0 || k >= 1);
             const double tl = fmax(-lo[j], p.t_min), th = fmax(hi[j], p.t_min);
             if (act) r0 = fmax(r0, fmax(tl + lo[j], th - hi[j]));
-            const double rl = 1.0 / tl, rh = 1.0 / th;
+            const double rl = rcp(tl), rh = rcp(th);
             st.t(ls, 2 * j) = act ? tl : 1.0;
             st.t(ls, 2 * j + 1) = act ? th : 1.0;
             st.rt(ls, 2 * j) = act ? rl : 1.0;
