@@ -97,6 +97,24 @@ def main():
         U.append(r["u0"][0].copy())
         X.append(xs[0].copy())
     np.savez_compressed(os.path.join(HERE, "config1_rti_full.npz"), U=np.array(U), X=np.array(X))
+
+    # 6. main.m as the reference runs it: santal, Hp = 10 (main.m:41), the 'sqp' +
+    #    'merit_backtracking' options of create_ocp_opts (max_iter 30, tol 1e-6), 201 steps
+    N = 10
+    op = make_opts(N=N, sqp_iters=30, nlp_mode=1)
+    warm = orc.new_warm(1, N)
+    xs = np.zeros((1, 4))
+    U, X, ST, IT = [], [xs[0].copy()], [], []
+    for i in range(1, T + 1):
+        r = orc.controller_solve(op, xs, traj, i, warm)
+        fx, _ = orc.dynamics(xs, r["u0"])
+        xs = xs + 0.05 * fx
+        U.append(r["u0"][0].copy())
+        X.append(xs[0].copy())
+        ST.append(int(r["status"][0]))
+        IT.append(int(r["iters"][0]))
+    np.savez_compressed(os.path.join(HERE, "main_m_sqp_closed_loop.npz"), U=np.array(U), X=np.array(X),
+                        status=np.array(ST, np.int32), iters=np.array(IT, np.int32))
     print("golden fixtures written to", HERE, "stable lanes:", int(stable.sum()), "/", nb)
 
 

@@ -86,3 +86,20 @@ def test_closed_loop_config1_rti_full():
         np.testing.assert_allclose(r["U"][lane], g["U"], rtol=0, atol=1e-8)
         np.testing.assert_allclose(r["X"][lane], g["X"], rtol=0, atol=1e-8)
     assert np.all(r["status"] == 0)
+
+
+def test_closed_loop_main_m_sqp():
+    """main.m's own controller (Hp = 10, 'sqp' + 'merit_backtracking', max_iter 30), 201 steps
+    on the device in one call, against the committed oracle trace."""
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    g = np.load(os.path.join(GOLDEN, "main_m_sqp_closed_loop.npz"))
+    s = OcpSolver(N=10, batch=3, sqp_iters=30, nlp_solver_type="SQP")
+    s.set_shapes([make_shape("santal")])
+    s.set_reference_trajectory(straight_traj())
+    r = s.closed_loop(np.zeros(4), 201)
+    s.close()
+    for lane in range(3):
+        np.testing.assert_allclose(r["U"][lane], g["U"], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(r["X"][lane], g["X"], rtol=0, atol=1e-7)
+        assert np.mean(r["status"][lane] == g["status"]) > 0.95

@@ -257,3 +257,19 @@ def test_config1_rti_full_golden(oracle):
         xs = xs + 0.05 * fx
     np.testing.assert_allclose(xs[0], g["X"][-1], atol=1e-12)
     assert abs(xs[0, 0] - 0.1) < 2e-3                       # reaches the 0.10 m waypoint
+
+
+def test_main_m_sqp_closed_loop_golden(oracle):
+    """main.m's own setup (Hp = 10, merit-backtracking SQP, max_iter 30), 201 steps."""
+    g = np.load(os.path.join(GOLDEN, "main_m_sqp_closed_loop.npz"))
+    op = make_opts(N=10, sqp_iters=30, nlp_mode=1)
+    warm = oracle.new_warm(1, 10)
+    xs = np.zeros((1, 4))
+    traj = straight_traj()
+    for i in range(1, 202):
+        r = oracle.controller_solve(op, xs, traj, i, warm)
+        np.testing.assert_allclose(r["u0"][0], g["U"][i - 1], rtol=0, atol=1e-12)
+        assert r["status"][0] == g["status"][i - 1] and r["iters"][0] == g["iters"][i - 1]
+        fx, _ = oracle.dynamics(xs, r["u0"])
+        xs = xs + 0.05 * fx
+    assert np.mean(g["status"] == 0) > 0.8 and abs(xs[0, 0] - 0.1) < 2e-3
