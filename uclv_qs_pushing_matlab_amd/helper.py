@@ -3,8 +3,9 @@
 The whole loop — controller solve, Euler plant step with evalModelVariableShape, optional
 sim_noise — runs on the GPU through qsp_closed_loop; one host round trip per call.
 Not reproduced: the disturbance branch (:221-236, needs MATLAB's fminunc to re-locate the
-contact point), print/debug_cost (MATLAB figures) and the plant delay buffer (delay 0 in
-every reference configuration).
+contact point; main.m sets t_dist = 15/0.05 = 300 > the 201 steps of its 10 s run, so the
+branch never fires there), print/debug_cost (MATLAB figures) and the plant delay buffer
+(delay 0 in every reference configuration).
 """
 import numpy as np
 
