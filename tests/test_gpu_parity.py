@@ -231,3 +231,28 @@ def test_decagon_spline_matches_oracle():
     np.testing.assert_allclose(C, Co, rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(D, Do, rtol=1e-11, atol=1e-12)
     np.testing.assert_allclose(Dd, dDo, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("N,S", [(1, 0), (2, 0), (5, 0), (5, 2), (20, 2), (31, 0), (63, 1), (64, 0), (90, 2)])
+def test_horizon_and_layout_edges(oracle, N, S):
+    """Odd/even horizons, padding slots (S = 2 with N + 1 odd), a group filling the whole
+    wavefront (N = 63, S = 1), two stages per lane beyond it: GPU = oracle at K = 2."""
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    nb, K = 13, 2
+    x0 = config2_x0(nb, 100 + N)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K, stages_per_lane=S)
+    s.set_shapes([make_shape(n) for n in NAMES], shape_id=sid)
+    s.set_reference_trajectory(traj)
+    u = s.controller_solve(x0, 1)
+    X = s.get("x")
+    st = s.get("status")
+    s.close()
+    w = oracle.new_warm(nb, N)
+    r = oracle.controller_solve(make_opts(N=N, sqp_iters=K), x0, traj, 1, w, shape_id=sid)
+    assert np.all(st == 0)
+    np.testing.assert_allclose(u, r["u0"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(X, w["X"].reshape(nb, N + 1, 4), rtol=0, atol=1e-9)
