@@ -80,3 +80,17 @@ def test_helper_closed_loop_mirror():
     np.testing.assert_allclose(np.stack([u_n[0, :20], u_t[0, :20]], 1), gold["u0"], atol=1e-9)
     # the slider tracks the 0.01 m/s line
     assert abs(out[0][0, -1] - 0.01 * 10.0) < 0.02
+
+
+def test_acados_timing_fields():
+    """get('time_tot'/'time_lin'/'time_qp_sol') as helper.m:264-269 prints them."""
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    from conftest import straight_traj
+    s = OcpSolver(N=20, batch=64, sqp_iters=5, timings=True)
+    s.set_shapes([make_shape("santal")])
+    s.set_reference_trajectory(straight_traj())
+    s.controller_solve(np.zeros((64, 4)), 1)
+    tt, tl, tq = s.get("time_tot"), s.get("time_lin"), s.get("time_qp_sol")
+    s.close()
+    assert 0 < tl < tt and 0 < tq < tt and tl + tq <= tt * 1.05

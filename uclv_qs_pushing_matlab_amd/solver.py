@@ -23,7 +23,8 @@ class OcpSolver:
 
     def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
                  cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10,
-                 nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
+                 nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
+                 timings=False):
         L = _lib.lib()
         o = _lib.Options()
         L.qsp_default_options(C.byref(o))
@@ -54,6 +55,9 @@ class OcpSolver:
         self._uh = np.array([0.011, 0.03, 0.05])
         self._dirty = set(["x0", "yref", "init"])
         self.n_shapes = 0
+        # timings=True: per-kernel HIP events around every solve, for get('time_lin'/'time_qp_sol')
+        self._timings = bool(timings)
+        self._last_times = None
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -166,9 +170,16 @@ class OcpSolver:
                   "qsp_set_init")
         self._dirty.clear()
 
+    def _timed(self, fn, *args):
+        if self._timings:
+            self.set_kernel_timing(1)
+        fn(*args)
+        if self._timings:
+            self._last_times = self.kernel_times()
+
     def solve(self):
         self._flush()
-        check(self._L.qsp_solve(self._h), "qsp_solve")
+        self._timed(lambda: check(self._L.qsp_solve(self._h), "qsp_solve"))
 
     # ----------------------------------------------------------------- get
     def get(self, field, stage=None):
@@ -189,6 +200,11 @@ class OcpSolver:
             ms = C.c_double()
             check(self._L.qsp_get_time_tot(self._h, C.byref(ms)), "get('time_tot')")
             return ms.value * 1e-3
+        if field in ("time_lin", "time_qp_sol"):                # helper.m:264-269, seconds
+            if self._last_times is None:
+                raise KeyError(f"get('{field}') needs OcpSolver(..., timings=True) and a solve")
+            key = "linearize" if field == "time_lin" else "qp_step"
+            return self._last_times[key][0] * 1e-3
         raise KeyError(f"OcpSolver.get: unknown field '{field}'")
 
     def get_u0(self):
@@ -239,7 +255,7 @@ class OcpSolver:
     def controller_solve(self, x0, index_time):
         x0 = f64(self._lanes(x0, 4))
         idx = i32(np.broadcast_to(np.asarray(index_time, np.int32), (self.B,)))
-        check(self._L.qsp_controller_solve(self._h, ptr(x0), ptr(idx)), "qsp_controller_solve")
+        self._timed(lambda: check(self._L.qsp_controller_solve(self._h, ptr(x0), ptr(idx)), "qsp_controller_solve"))
         return self.get_u0()
 
     def closed_loop(self, x0, n_steps, index0=1, noise=None):
