@@ -96,10 +96,10 @@ enum LdsField : int {
     F_DU = 15,    // 2  damped QP control step
     F_VA = 17,    // 3  affine-predictor bounded components (ds, dun, dut)
     F_VN = 20,    // 3  corrector bounded components
-    F_DX = 23,    // 4  final QP state step
-    F_HG = 27,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
-    F_RT = 33,    // 6  1 / slack, refreshed whenever the slacks change
-    F_COUNT = 39
+    F_DX = 17,    // 4  final QP state step (written after the IPM: aliases F_VA / F_VN)
+    F_HG = 23,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
+    F_RT = 29,    // 6  1 / slack, refreshed whenever the slacks change
+    F_COUNT = 35
 };
 template <int S>
 constexpr int lds_bytes() { return F_COUNT * S * BLOCK * 8; }
@@ -390,28 +390,24 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         }
     }
     for (int j = c.L - 1; j >= 0; --j) {
-        const bool act = (c.lig == j);
+        // Lanes above j already hold their final factors and sit the step out (exec
+        // mask); lanes below j compute a throw-away step that their own turn overwrites.
+        // Writing the factors in place this way needs no per-step selects.
+        if (c.lig <= j) {
 #pragma unroll
-        for (int ls = S - 1; ls >= 0; --ls) {
-            if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
-            const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], st.g[ls][3] + st.hg(ls, 3)};
-            const double gu[2] = {st.g[ls][4] + st.hg(ls, 4), st.g[ls][5] + st.hg(ls, 5)};
-            double K[8], Ri[3], Pb[4], kk[2];
-            if (FACTOR) {
-                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg(ls, 0)};
-                const double Hu[2] = {p.tau * p.W[4] + st.hg(ls, 1), p.tau * p.W[5] + st.hg(ls, 2)};
-                ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, P, pv, K, Ri, Pb, kk);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) st.K[ls][q] = act ? K[q] : st.K[ls][q];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) st.Ri[ls][q] = act ? Ri[q] : st.Ri[ls][q];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) st.Pb[ls][q] = act ? Pb[q] : st.Pb[ls][q];
-            } else {
-                ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Ri[ls], st.Pb[ls], pv, kk);
+            for (int ls = S - 1; ls >= 0; --ls) {
+                if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
+                const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], st.g[ls][3] + st.hg(ls, 3)};
+                const double gu[2] = {st.g[ls][4] + st.hg(ls, 4), st.g[ls][5] + st.hg(ls, 5)};
+                if (FACTOR) {
+                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg(ls, 0)};
+                    const double Hu[2] = {p.tau * p.W[4] + st.hg(ls, 1), p.tau * p.W[5] + st.hg(ls, 2)};
+                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, P, pv, st.K[ls], st.Ri[ls],
+                                    st.Pb[ls], st.kk[ls]);
+                } else {
+                    ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Ri[ls], st.Pb[ls], pv, st.kk[ls]);
+                }
             }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) st.kk[ls][q] = act ? kk[q] : st.kk[ls][q];
         }
         if (FACTOR) {
 #pragma unroll
@@ -894,7 +890,9 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
     // frozen instances (converged in nlp_mode 1, or a failed QP earlier) are not iterated
     const bool was_done = A.wdone && A.wdone[iv] != 0;
-    bool skip = was_done;
+    // padding lanes (no instance) must not hold their wave in the IPM loop: they mirror
+    // instance B-1 with group reductions over foreign lanes and need not converge
+    bool skip = was_done || !c.real;
     if constexpr (MERIT) {
         static_assert(S == 1, "nlp_mode 1 uses one stage per lane");
         // nlp_mode 1: KKT test of the current iterate; converged instances freeze
