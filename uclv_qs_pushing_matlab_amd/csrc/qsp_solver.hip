@@ -110,7 +110,7 @@ struct Stage {
     double a[S][6];          // free entries of A_k (qsp_math.hpp rk4)
     double B[S][8];
     double bb[S][4];         // defect phi(x_k,u_k) - x_{k+1}
-    double K[S][8], Ri[S][3], Pb[S][4], kk[S][2];
+    double K[S][8], Rn[S][3], Pb[S][4], kk[S][2];   // Rn = -R~^-1
     double* lds;             // this thread's column of the workgroup's LDS block
     __device__ __forceinline__ double& f(int field, int ls, int i) const { return lds[((field + i) * S + ls) * BLOCK]; }
     __device__ __forceinline__ double& t(int ls, int q) const { return f(F_T, ls, q); }
@@ -148,6 +148,14 @@ __device__ __forceinline__ double wave_from_next(double v) {   // lane i <- lane
     const int hi = __builtin_amdgcn_update_dpp(h, h, 0x130, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
+// lane i <- lane i+1's v; lanes without a source keep `old`.  With old = the value
+// the register held before the step, a hand-over inside a divergent region needs no
+// extra copy to merge the lanes that sat the step out.
+__device__ __forceinline__ double wave_from_next(double old, double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_from_prev(double v) {   // lane i <- lane i-1
     const int l = __double2loint(v), h = __double2hiint(v);
     const int lo = __builtin_amdgcn_update_dpp(l, l, 0x138, 0xf, 0xf, false);
@@ -171,7 +179,7 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
                                                 const double Hx[4], const double Hu[2],
                                                 const double gx[4], const double gu[2],
                                                 double P[10], double pv[4],
-                                                double K[8], double Ri[3], double Pb[4], double kk[2]) {
+                                                double K[8], double Rn[3], double Pb[4], double kk[2]) {
     // full symmetric P
     double Pm[4][4];
 #pragma unroll
@@ -235,17 +243,18 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     qt[1] = gx[1] + pp[1];
     qt[2] = gx[2] + (a[0] * pp[0] + a[2] * pp[1] + pp[2]);
     qt[3] = gx[3] + (a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3]);
-    // R~^-1
+    // Rn = -R~^-1 (kept negated: the sign folds into the multiplies, bit-identical to
+    // negating the products afterwards)
     const double idet = rcp(R00 * R11 - R01 * R01);
-    Ri[0] = R11 * idet; Ri[1] = -R01 * idet; Ri[2] = R00 * idet;
+    Rn[0] = (-R11) * idet; Rn[1] = R01 * idet; Rn[2] = (-R00) * idet;
     // K = -R~^-1 S~ ; kk = -R~^-1 r~
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        K[j] = -(Ri[0] * St[0][j] + Ri[1] * St[1][j]);
-        K[4 + j] = -(Ri[1] * St[0][j] + Ri[2] * St[1][j]);
+        K[j] = Rn[0] * St[0][j] + Rn[1] * St[1][j];
+        K[4 + j] = Rn[1] * St[0][j] + Rn[2] * St[1][j];
     }
-    kk[0] = -(Ri[0] * rt[0] + Ri[1] * rt[1]);
-    kk[1] = -(Ri[1] * rt[0] + Ri[2] * rt[1]);
+    kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
+    kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
     // P = Q~ + S~'K ; p = q~ + K'r~
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -257,7 +266,7 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
 
 // Vector-only backward step reusing the factorisation (Mehrotra corrector).
 __device__ __forceinline__ void ric_vector_step(const double a[6], const double B[8], const double gx[4], const double gu[2],
-                                                const double K[8], const double Ri[3], const double Pb[4],
+                                                const double K[8], const double Rn[3], const double Pb[4],
                                                 double pv[4], double kk[2]) {
     double pp[4];
 #pragma unroll
@@ -270,8 +279,8 @@ __device__ __forceinline__ void ric_vector_step(const double a[6], const double 
     qt[1] = gx[1] + pp[1];
     qt[2] = gx[2] + (a[0] * pp[0] + a[2] * pp[1] + pp[2]);
     qt[3] = gx[3] + (a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3]);
-    kk[0] = -(Ri[0] * rt[0] + Ri[1] * rt[1]);
-    kk[1] = -(Ri[1] * rt[0] + Ri[2] * rt[1]);
+    kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
+    kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[i] = qt[i] + (K[i] * rt[0] + K[4 + i] * rt[1]);
 }
@@ -393,7 +402,13 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         // Lanes above j already hold their final factors and sit the step out (exec
         // mask); lanes below j compute a throw-away step that their own turn overwrites.
         // Writing the factors in place this way needs no per-step selects.
+        // The hand-over runs inside the same region: lane j-1 (active) reads lane j (active).
         if (c.lig <= j) {
+            double Pc[10], pvc[4];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) Pc[i] = P[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pvc[i] = pv[i];
 #pragma unroll
             for (int ls = S - 1; ls >= 0; --ls) {
                 if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
@@ -402,19 +417,19 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 if (FACTOR) {
                     const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg(ls, 0)};
                     const double Hu[2] = {p.tau * p.W[4] + st.hg(ls, 1), p.tau * p.W[5] + st.hg(ls, 2)};
-                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, P, pv, st.K[ls], st.Ri[ls],
+                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, Pc, pvc, st.K[ls], st.Rn[ls],
                                     st.Pb[ls], st.kk[ls]);
                 } else {
-                    ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Ri[ls], st.Pb[ls], pv, st.kk[ls]);
+                    ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Rn[ls], st.Pb[ls], pvc, st.kk[ls]);
                 }
             }
-        }
-        if (FACTOR) {
+            if (FACTOR) {
 #pragma unroll
-            for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i]);
-        }
+                for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i], Pc[i]);
+            }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i]);
+            for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
+        }
     }
     // forward: every slot of lanes 0 .. L-2 is a stage k < N; the last lane holds lsN of them
     double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
