@@ -175,6 +175,8 @@ __device__ __forceinline__ void ric_terminal(const SolveParams& p, const double 
 
 // One backward factorisation step exploiting A = [[1,0,a0,a1],[0,1,a2,a3],[0,0,1,a4],[0,0,0,a5]].
 // Hx, Hu: diagonal stage Hessian (incl. barrier); gx, gu: gradient (incl. barrier).
+// Every sum is written as one left-to-right chain starting from its additive term, so
+// each product contracts into an FMA (no separate multiply + add per sum).
 __device__ __forceinline__ void ric_factor_step(const double a[6], const double B[8], const double bb[4],
                                                 const double Hx[4], const double Hu[2],
                                                 const double gx[4], const double gu[2],
@@ -186,13 +188,13 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) Pm[i][j] = P[sidx(i, j)];
-    // PA
+    // PA (columns 0, 1 of A are e0, e1)
     double PA[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         PA[i][0] = Pm[i][0];
         PA[i][1] = Pm[i][1];
-        PA[i][2] = Pm[i][0] * a[0] + Pm[i][1] * a[2] + Pm[i][2];
+        PA[i][2] = Pm[i][2] + Pm[i][0] * a[0] + Pm[i][1] * a[2];
         PA[i][3] = Pm[i][0] * a[1] + Pm[i][1] * a[3] + Pm[i][2] * a[4] + Pm[i][3] * a[5];
     }
     // PB
@@ -210,41 +212,38 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
         pp[i] = pv[i] + Pb[i];
     }
     // R~ = Hu + B'PB (sym), S~ = B'PA (2x4), r~ = gu + B'pp
-    double R00 = Hu[0] + (B[0] * PB[0][0] + B[2] * PB[1][0] + B[4] * PB[2][0] + B[6] * PB[3][0]);
-    double R01 = B[0] * PB[0][1] + B[2] * PB[1][1] + B[4] * PB[2][1] + B[6] * PB[3][1];
-    double R11 = Hu[1] + (B[1] * PB[0][1] + B[3] * PB[1][1] + B[5] * PB[2][1] + B[7] * PB[3][1]);
+    const double R00 = Hu[0] + B[0] * PB[0][0] + B[2] * PB[1][0] + B[4] * PB[2][0] + B[6] * PB[3][0];
+    const double R01 = B[0] * PB[0][1] + B[2] * PB[1][1] + B[4] * PB[2][1] + B[6] * PB[3][1];
+    const double R11 = Hu[1] + B[1] * PB[0][1] + B[3] * PB[1][1] + B[5] * PB[2][1] + B[7] * PB[3][1];
     // S~ = B'PA = (PB)'A with the structure of A
     double St[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         St[i][0] = PB[0][i];
         St[i][1] = PB[1][i];
-        St[i][2] = PB[0][i] * a[0] + PB[1][i] * a[2] + PB[2][i];
+        St[i][2] = PB[2][i] + PB[0][i] * a[0] + PB[1][i] * a[2];
         St[i][3] = PB[0][i] * a[1] + PB[1][i] * a[3] + PB[2][i] * a[4] + PB[3][i] * a[5];
     }
     double rt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + (B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3]);
+    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3];
     // Q~ = Hx + A'PA  (upper triangle), q~ = gx + A'pp
     double Qt[10];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const double c0 = PA[0][j], c1 = PA[1][j], c2 = PA[2][j], c3 = PA[3][j];
-        const double r2 = a[0] * c0 + a[2] * c1 + c2;
-        const double r3 = a[1] * c0 + a[3] * c1 + a[4] * c2 + a[5] * c3;
         if (j >= 0) Qt[sidx(0, j)] = c0;
         if (j >= 1) Qt[sidx(1, j)] = c1;
-        if (j >= 2) Qt[sidx(2, j)] = r2;
-        if (j >= 3) Qt[sidx(3, j)] = r3;
+        if (j >= 2) Qt[sidx(2, j)] = (j == 2 ? Hx[2] + c2 : c2) + a[0] * c0 + a[2] * c1;
+        if (j >= 3) Qt[sidx(3, j)] = Hx[3] + a[1] * c0 + a[3] * c1 + a[4] * c2 + a[5] * c3;
     }
-    Qt[0] += Hx[0]; Qt[4] += Hx[1]; Qt[7] += Hx[2]; Qt[9] += Hx[3];
+    Qt[0] += Hx[0]; Qt[4] += Hx[1];
     double qt[4];
     qt[0] = gx[0] + pp[0];
     qt[1] = gx[1] + pp[1];
-    qt[2] = gx[2] + (a[0] * pp[0] + a[2] * pp[1] + pp[2]);
-    qt[3] = gx[3] + (a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3]);
-    // Rn = -R~^-1 (kept negated: the sign folds into the multiplies, bit-identical to
-    // negating the products afterwards)
+    qt[2] = gx[2] + pp[2] + a[0] * pp[0] + a[2] * pp[1];
+    qt[3] = gx[3] + a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3];
+    // Rn = -R~^-1 (kept negated: the sign folds into the multiplies)
     const double idet = rcp(R00 * R11 - R01 * R01);
     Rn[0] = (-R11) * idet; Rn[1] = R01 * idet; Rn[2] = (-R00) * idet;
     // K = -R~^-1 S~ ; kk = -R~^-1 r~
@@ -259,9 +258,9 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = i; j < 4; ++j) P[sidx(i, j)] = Qt[sidx(i, j)] + (St[0][i] * K[j] + St[1][i] * K[4 + j]);
+        for (int j = i; j < 4; ++j) P[sidx(i, j)] = Qt[sidx(i, j)] + St[0][i] * K[j] + St[1][i] * K[4 + j];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + (K[i] * rt[0] + K[4 + i] * rt[1]);
+    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
 }
 
 // Vector-only backward step reusing the factorisation (Mehrotra corrector).
@@ -273,25 +272,25 @@ __device__ __forceinline__ void ric_vector_step(const double a[6], const double 
     for (int i = 0; i < 4; ++i) pp[i] = pv[i] + Pb[i];
     double rt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + (B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3]);
+    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3];
     double qt[4];
     qt[0] = gx[0] + pp[0];
     qt[1] = gx[1] + pp[1];
-    qt[2] = gx[2] + (a[0] * pp[0] + a[2] * pp[1] + pp[2]);
-    qt[3] = gx[3] + (a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3]);
+    qt[2] = gx[2] + pp[2] + a[0] * pp[0] + a[2] * pp[1];
+    qt[3] = gx[3] + a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3];
     kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
     kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + (K[i] * rt[0] + K[4 + i] * rt[1]);
+    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
 }
 
 // dx_{k+1} = A dx + B du + b
 __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], const double bb[4],
                                          const double du[2], double dx[4]) {
-    const double n0 = bb[0] + ((dx[0] + a[0] * dx[2] + a[1] * dx[3]) + (B[0] * du[0] + B[1] * du[1]));
-    const double n1 = bb[1] + ((dx[1] + a[2] * dx[2] + a[3] * dx[3]) + (B[2] * du[0] + B[3] * du[1]));
-    const double n2 = bb[2] + ((dx[2] + a[4] * dx[3]) + (B[4] * du[0] + B[5] * du[1]));
-    const double n3 = bb[3] + ((a[5] * dx[3]) + (B[6] * du[0] + B[7] * du[1]));
+    const double n0 = bb[0] + dx[0] + a[0] * dx[2] + a[1] * dx[3] + B[0] * du[0] + B[1] * du[1];
+    const double n1 = bb[1] + dx[1] + a[2] * dx[2] + a[3] * dx[3] + B[2] * du[0] + B[3] * du[1];
+    const double n2 = bb[2] + dx[2] + a[4] * dx[3] + B[4] * du[0] + B[5] * du[1];
+    const double n3 = bb[3] + a[5] * dx[3] + B[6] * du[0] + B[7] * du[1];
     dx[0] = n0; dx[1] = n1; dx[2] = n2; dx[3] = n3;
 }
 
@@ -439,8 +438,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         for (int ls = 0; ls < S; ++ls) {
             if (j == c.L - 1 && ls >= lsN) continue;
             double du[2];
-            du[0] = st.kk[ls][0] + (st.K[ls][0] * dx[0] + st.K[ls][1] * dx[1] + st.K[ls][2] * dx[2] + st.K[ls][3] * dx[3]);
-            du[1] = st.kk[ls][1] + (st.K[ls][4] * dx[0] + st.K[ls][5] * dx[1] + st.K[ls][6] * dx[2] + st.K[ls][7] * dx[3]);
+            du[0] = st.kk[ls][0] + st.K[ls][0] * dx[0] + st.K[ls][1] * dx[1] + st.K[ls][2] * dx[2] + st.K[ls][3] * dx[3];
+            du[1] = st.kk[ls][1] + st.K[ls][4] * dx[0] + st.K[ls][5] * dx[1] + st.K[ls][6] * dx[2] + st.K[ls][7] * dx[3];
             if (act) {
                 st.f(out, ls, 0) = dx[3];
                 st.f(out, ls, 1) = du[0];
