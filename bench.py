@@ -203,6 +203,8 @@ def main():
     qp_ms, qp_n = ktimes["qp_step"]
     qp_avg_s = qp_ms / max(qp_n, 1) * 1e-3
     qp_flops_launch = float(qp_iter.astype(np.float64).sum()) * N * FLOP_IPM_STAGE / K
+    if args.nlp == "SQP_RTI":   # the SQP iteration's linearisation runs inside the qp_step launch
+        qp_flops_launch += float(Bl) * N * FLOP_LIN_STAGE
     if dist:
         tt = torch.tensor([float(np.count_nonzero(status))], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)

@@ -176,7 +176,9 @@ int qsp_synchronize(qsp_solver* s);
  * HIP events for the next n solves (0 disables): every kernel boundary of each solve is then
  * recorded on the solve's stream.  qsp_get_kernel_times synchronises the recorded events and
  * returns the summed milliseconds and launch counts per kernel family in the order
- * {prologue, linearize, qp_step, epilogue}, then re-arms the pool. */
+ * {prologue, linearize, qp_step, epilogue}, then re-arms the pool.  With nlp_mode 0 the SQP
+ * iteration's linearisation runs inside the qp_step kernel, so "linearize" is only the
+ * wave-packing sort before it; with nlp_mode 1 it is the separate linearisation kernel. */
 int qsp_set_kernel_timing(qsp_solver* s, int32_t max_solves);
 int qsp_get_kernel_times(qsp_solver* s, double* ms /* 4 */, int32_t* launches /* 4 */);
 

@@ -93,4 +93,5 @@ def test_acados_timing_fields():
     s.controller_solve(np.zeros((64, 4)), 1)
     tt, tl, tq = s.get("time_tot"), s.get("time_lin"), s.get("time_qp_sol")
     s.close()
-    assert 0 < tl < tt and 0 < tq < tt and tl + tq <= tt * 1.05
+    # nlp_mode 0 linearises inside the qp_step kernel: time_lin is the wave-packing sort only
+    assert 0 <= tl < tt and 0 < tq < tt and tl + tq <= tt * 1.05

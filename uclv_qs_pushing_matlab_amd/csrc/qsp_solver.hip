@@ -853,7 +853,7 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
     return rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
 }
 
-template <int S, bool MERIT = false>
+template <int S, bool MERIT = false, bool LIN = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -886,15 +886,49 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         const int k = kof<S>(c, ls);
         const int kc = k <= N ? k : N;
         const int ku = k < N ? k : N - 1;
-        const double* in = A.wlin + (size_t)iv * (N + 1) + kc;
+        if constexpr (LIN) {
+            // fused linearisation (linearize_kernel's arithmetic, one stage per slot): the
+            // stage data stays in registers instead of a 24-double HBM round trip
+            if (kc < N) {
+                const double xk[4] = {X[4 * kc], X[4 * kc + 1], X[4 * kc + 2], X[4 * kc + 3]};
+                const double uk[2] = {U[2 * kc], U[2 * kc + 1]};
+                Lin Ln;
+                rk4<true>(shape_of(A, iv), p.Ts, xk, uk, Ln);
+                const double* yr = A.yref + ((size_t)iv * N + kc) * 6;
 #pragma unroll
-        for (int q = 0; q < 6; ++q) st.a[ls][q] = in[(L_A + q) * tot];
+                for (int q = 0; q < 6; ++q) st.a[ls][q] = Ln.a[q];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) st.B[ls][q] = in[(L_B + q) * tot];
+                for (int q = 0; q < 8; ++q) st.B[ls][q] = Ln.B[q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st.bb[ls][q] = in[(L_BB + q) * tot];
+                for (int q = 0; q < 4; ++q) st.bb[ls][q] = Ln.xn[q] - X[4 * (kc + 1) + q];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) st.g[ls][q] = in[(L_G + q) * tot];
+                for (int q = 0; q < 4; ++q) st.g[ls][q] = p.tau * p.W[q] * (xk[q] - yr[q]);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) st.g[ls][4 + q] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
+            } else {
+                const double* ye = A.yref_e + (size_t)iv * 4;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) st.a[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st.B[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.bb[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.g[ls][q] = p.We[q] * (X[4 * N + q] - ye[q]);
+                st.g[ls][4] = 0.0;
+                st.g[ls][5] = 0.0;
+            }
+        } else {
+            const double* in = A.wlin + (size_t)iv * (N + 1) + kc;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) st.a[ls][q] = in[(L_A + q) * tot];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) st.B[ls][q] = in[(L_B + q) * tot];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st.bb[ls][q] = in[(L_BB + q) * tot];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) st.g[ls][q] = in[(L_G + q) * tot];
+        }
         st.v(ls, 0) = X[4 * kc + 3];
         st.v(ls, 1) = U[2 * ku];
         st.v(ls, 2) = U[2 * ku + 1];
@@ -1350,7 +1384,9 @@ __global__ void vbound_kernel(const ShapeDev* shapes, const int32_t* sid, int n,
 }
 
 // ------------------------------------------------------------------ launchers
-template <int S>
+// LIN: the SQP iteration's linearisation runs inside the QP kernel (nlp_mode 0); without
+// it the kernel reads the stage data the workspace holds (qsp_qp_solve).
+template <int S, bool LIN>
 static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
@@ -1358,18 +1394,18 @@ static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream)
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)qp_step_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_bytes<S>());
+        (void)hipFuncSetAttribute((const void*)qp_step_kernel<S, false, LIN>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<S>());
         attr = true;
     }
-    hipLaunchKernelGGL(qp_step_kernel<S>, dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
+    hipLaunchKernelGGL((qp_step_kernel<S, false, LIN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
     return hipGetLastError();
 }
 
-static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream) {
+static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
-        case 1: return launch_qp_step<1>(a, it, stream);
-        case 2: return launch_qp_step<2>(a, it, stream);
+        case 1: return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
+        case 2: return lin ? launch_qp_step<2, true>(a, it, stream) : launch_qp_step<2, false>(a, it, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1416,11 +1452,13 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
             e = hipGetLastError();
             if (e != hipSuccess) break;
         }
-        hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
-        e = hipGetLastError();
+        const bool merit = a.p.nlp_mode == 1;
+        if (merit) {   // the line search reads the stage data too: linearise into the workspace
+            hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
+            e = hipGetLastError();
+        }
         if (e == hipSuccess) e = mark();
-        if (e == hipSuccess)
-            e = a.p.nlp_mode == 1 ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it, stream);
+        if (e == hipSuccess) e = merit ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it, stream, true);
         if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;
@@ -1431,7 +1469,9 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
 }
 
 // One QP (qsp_qp_solve): the workspace already holds the stage data.
-hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) { return launch_qp_any(a, S, a.p.sqp_iters - 1, stream); }
+hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) {
+    return launch_qp_any(a, S, a.p.sqp_iters - 1, stream, false);
+}
 
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,
                          double* Dd, double* kappa, hipStream_t stream) {
