@@ -110,7 +110,7 @@ struct Stage {
     double a[S][6];          // free entries of A_k (qsp_math.hpp rk4)
     double B[S][8];
     double bb[S][4];         // defect phi(x_k,u_k) - x_{k+1}
-    double K[S][8], Rn[S][3], Pb[S][4], kk[S][2];   // Rn = -R~^-1
+    double K[S][8], Rn[S][3], kk[S][2];   // Rn = -R~^-1
     double* lds;             // this thread's column of the workgroup's LDS block
     __device__ __forceinline__ double& f(int field, int ls, int i) const { return lds[((field + i) * S + ls) * BLOCK]; }
     __device__ __forceinline__ double& t(int ls, int q) const { return f(F_T, ls, q); }
@@ -181,7 +181,7 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
                                                 const double Hx[4], const double Hu[2],
                                                 const double gx[4], const double gu[2],
                                                 double P[10], double pv[4],
-                                                double K[8], double Rn[3], double Pb[4], double kk[2]) {
+                                                double K[8], double Rn[3], double kk[2]) {
     // full symmetric P
     double Pm[4][4];
 #pragma unroll
@@ -204,13 +204,10 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
 #pragma unroll
         for (int j = 0; j < 2; ++j)
             PB[i][j] = Pm[i][0] * B[j] + Pm[i][1] * B[2 + j] + Pm[i][2] * B[4 + j] + Pm[i][3] * B[6 + j];
-    // Pb, pp = p + P b
+    // pp = p + P b
     double pp[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        Pb[i] = Pm[i][0] * bb[0] + Pm[i][1] * bb[1] + Pm[i][2] * bb[2] + Pm[i][3] * bb[3];
-        pp[i] = pv[i] + Pb[i];
-    }
+    for (int i = 0; i < 4; ++i) pp[i] = pv[i] + Pm[i][0] * bb[0] + Pm[i][1] * bb[1] + Pm[i][2] * bb[2] + Pm[i][3] * bb[3];
     // R~ = Hu + B'PB (sym), S~ = B'PA (2x4), r~ = gu + B'pp
     const double R00 = Hu[0] + B[0] * PB[0][0] + B[2] * PB[1][0] + B[4] * PB[2][0] + B[6] * PB[3][0];
     const double R01 = B[0] * PB[0][1] + B[2] * PB[1][1] + B[4] * PB[2][1] + B[6] * PB[3][1];
@@ -263,23 +260,23 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
 }
 
-// Vector-only backward step reusing the factorisation (Mehrotra corrector).
-__device__ __forceinline__ void ric_vector_step(const double a[6], const double B[8], const double gx[4], const double gu[2],
-                                                const double K[8], const double Rn[3], const double Pb[4],
-                                                double pv[4], double kk[2]) {
-    double pp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pp[i] = pv[i] + Pb[i];
+// Vector-only backward step of the Mehrotra corrector, on the DIFFERENCE to the predictor:
+// the corrector changes only the gradient, by dg = (0, 0, 0, dgx3; dgu0, dgu1) (barrier
+// correction terms), and the recursion is linear in the gradient with the same factors, so
+//   dr = dgu + B' dp,  dq = dgx + A' dp,  dkk = Rn dr,  dp <- dq + K' dr,  dp_N = 0
+// (P b cancels in the difference; kk_corr = kk_pred + dkk).
+__device__ __forceinline__ void ric_delta_step(const double a[6], const double B[8], double dgx3, const double dgu[2],
+                                               const double K[8], const double Rn[3], double pv[4], double dkk[2]) {
     double rt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3];
+    for (int i = 0; i < 2; ++i) rt[i] = dgu[i] + B[i] * pv[0] + B[2 + i] * pv[1] + B[4 + i] * pv[2] + B[6 + i] * pv[3];
     double qt[4];
-    qt[0] = gx[0] + pp[0];
-    qt[1] = gx[1] + pp[1];
-    qt[2] = gx[2] + pp[2] + a[0] * pp[0] + a[2] * pp[1];
-    qt[3] = gx[3] + a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3];
-    kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
-    kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
+    qt[0] = pv[0];
+    qt[1] = pv[1];
+    qt[2] = pv[2] + a[0] * pv[0] + a[2] * pv[1];
+    qt[3] = dgx3 + a[1] * pv[0] + a[3] * pv[1] + a[4] * pv[2] + a[5] * pv[3];
+    dkk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
+    dkk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
 }
@@ -309,16 +306,18 @@ __device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
         const double sl = ll * rtl, sh = lh * rth;
-        double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
         if (CORR) {
+            // corrector: only the change of the gradient (ric_delta_step); the Hessian is the predictor's
             const double v = st.f(F_VA, ls, j);
             const double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
             const double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
             const double cl = smu - dtl * dll, ch = smu - dth * dlh;
-            gadd += ch * rth - cl * rtl;
+            st.hg(ls, 3 + j) = act ? ch * rth - cl * rtl : 0.0;
+        } else {
+            const double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
+            st.hg(ls, j) = act ? sl + sh : 0.0;
+            st.hg(ls, 3 + j) = act ? gadd : 0.0;
         }
-        st.hg(ls, j) = act ? sl + sh : 0.0;
-        st.hg(ls, 3 + j) = act ? gadd : 0.0;
     }
 }
 
@@ -372,8 +371,9 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
     }
 }
 
-// Backward pass over the group (factorisation or vector only), then forward pass
-// writing the bounded components of the solution into LDS field `out` (F_VA / F_VN).
+// Backward pass over the group (factorisation, or the corrector's difference recursion),
+// then forward pass writing the bounded components of the solution into LDS field `out`
+// (F_VA / F_VN).
 template <int S, bool FACTOR>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
                                               int out) {
@@ -387,14 +387,27 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
     // consumed by the neighbour after the hand-over.  The terminal stage k = N sits in
     // slot N % S of the last lane; the walk starts there.
     const int lsN = c.N - (c.L - 1) * S;
+    if (FACTOR) {
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls)
+            if (ls == lsN) ric_terminal(p, st.g[ls], P, pv);
+    }   // corrector difference: dp_N = 0
+    // the barrier-modified diagonal and gradient entries are fixed during the walk: formed
+    // once per slot instead of at every step
+    double hx3[S], hu[S][2], gx3[S], gu[S][2];
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
-        if (ls == lsN) {
-            if (FACTOR) ric_terminal(p, st.g[ls], P, pv);
-            else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) pv[i] = st.g[ls][i];
-            }
+        if (FACTOR) {
+            hx3[ls] = p.tau * p.W[3] + st.hg(ls, 0);
+            hu[ls][0] = p.tau * p.W[4] + st.hg(ls, 1);
+            hu[ls][1] = p.tau * p.W[5] + st.hg(ls, 2);
+            gx3[ls] = st.g[ls][3] + st.hg(ls, 3);
+            gu[ls][0] = st.g[ls][4] + st.hg(ls, 4);
+            gu[ls][1] = st.g[ls][5] + st.hg(ls, 5);
+        } else {
+            gx3[ls] = st.hg(ls, 3);
+            gu[ls][0] = st.hg(ls, 4);
+            gu[ls][1] = st.hg(ls, 5);
         }
     }
     for (int j = c.L - 1; j >= 0; --j) {
@@ -411,15 +424,19 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 #pragma unroll
             for (int ls = S - 1; ls >= 0; --ls) {
                 if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
-                const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], st.g[ls][3] + st.hg(ls, 3)};
-                const double gu[2] = {st.g[ls][4] + st.hg(ls, 4), st.g[ls][5] + st.hg(ls, 5)};
                 if (FACTOR) {
-                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], p.tau * p.W[3] + st.hg(ls, 0)};
-                    const double Hu[2] = {p.tau * p.W[4] + st.hg(ls, 1), p.tau * p.W[5] + st.hg(ls, 2)};
-                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, Hu, gx, gu, Pc, pvc, st.K[ls], st.Rn[ls],
-                                    st.Pb[ls], st.kk[ls]);
+                    const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], gx3[ls]};
+                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[ls]};
+                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, hu[ls], gx, gu[ls], Pc, pvc, st.K[ls],
+                                    st.Rn[ls], st.kk[ls]);
                 } else {
-                    ric_vector_step(st.a[ls], st.B[ls], gx, gu, st.K[ls], st.Rn[ls], st.Pb[ls], pvc, st.kk[ls]);
+                    double dkk[2];
+                    ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvc, dkk);
+                    // in place only on the lane's own turn (a throw-away step must not accumulate)
+                    if (c.lig == j) {
+                        st.kk[ls][0] += dkk[0];
+                        st.kk[ls][1] += dkk[1];
+                    }
                 }
             }
             if (FACTOR) {
