@@ -56,7 +56,7 @@ struct qsp_solver {
     int n_shapes = 0;
     DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
     DevBuf warm_valid, traj, index_time;
-    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit;
+    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit, whist;
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
@@ -182,6 +182,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wperm = s->wperm.as<int32_t>();
     if (s->poison) a.flags |= QSP_FLAG_POISON;
     a.wnit = s->wnit.as<int32_t>();
+    a.whist = s->whist.as<int32_t>();
     a.PI_in = s->PI.as<double>();   // 'init_pi' (solve) / shifted warm start (controller)
     return a;
 }
@@ -340,6 +341,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
+    al(s->whist, 4 * 64 * 4);
     al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);
@@ -379,7 +381,8 @@ int qsp_destroy(qsp_solver* s) {
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
-                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit};
+                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
+                      &s->whist};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
     for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);

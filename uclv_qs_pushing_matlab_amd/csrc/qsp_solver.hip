@@ -84,6 +84,10 @@ __device__ __forceinline__ int sidx(int i, int j) {
     return i == 0 ? j : (i == 1 ? 3 + j : (i == 2 ? 5 + j : 9));
 }
 
+// Wave-packing key of an instance from the IPM iteration count of its last QP: longest
+// first (LPT order), so a launch does not end on a tail of long waves.
+__device__ __forceinline__ int iters_key(int nit, int maxkey) { return maxkey - min(max(nit, 0), maxkey); }
+
 // ------------------------------------------------------------- per-lane state
 // Registers hold what the horizon recursions read on every step (stage model,
 // gradient, Riccati factors); LDS holds what only the stage-parallel phases touch
@@ -988,6 +992,12 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             A.sqp_iter[iv] = it;
         }
     }
+    if (A.whist && c.real && c.lig == 0) {
+        // wave-packing key of this instance for the next launch (sort_by_iters_kernel): the
+        // iteration count it records below (an instance that did not iterate keeps its old one)
+        const int rec = (MERIT || !(skip || failed)) ? nit : A.wnit[iv];
+        atomicAdd(&A.whist[(it & 1) * 64 + iters_key(rec, p.qp_iters)], 1);
+    }
     if constexpr (MERIT) {
         // QP solution (step, dynamics and bound multipliers) for the line-search kernel
         double piq[4];
@@ -1050,24 +1060,37 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 }
 
 // Counting sort of the instances by the IPM iteration count of their last QP (keys
-// 0..qp_iters): one workgroup; the order inside a key is arbitrary and does not affect
-// any result (instances are independent).
-__global__ void __launch_bounds__(1024) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm) {
-    __shared__ int hist[64];
-    __shared__ int off[64];
+// 0..qp_iters), in one pass over the instances: the histogram of the keys was accumulated
+// by the QP launch itself (whist, parity q), each block places its instances at the key's
+// prefix plus a block offset taken from the running counters, then clears the other
+// parity's histogram and counters for the next launch.  The order inside a key is
+// arbitrary and does not affect any result (instances are independent).
+__global__ void __launch_bounds__(256) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm,
+                                                            int32_t* whist, int q) {
+    __shared__ int pre[64], lcount[64], lbase[64];
     const int tid = threadIdx.x;
-    if (tid < 64) hist[tid] = 0;
-    __syncthreads();
-    // longest first: the waves with the most IPM iterations start first (LPT order), so the
-    // launch does not end on a tail of long waves
-    for (int i = tid; i < B; i += blockDim.x) atomicAdd(&hist[maxkey - min(max(nit[i], 0), maxkey)], 1);
-    __syncthreads();
+    int32_t* hist = whist + q * 64;
+    int32_t* run = whist + 128 + q * 64;
+    if (tid < 64) lcount[tid] = 0;
     if (tid == 0) {
         int acc = 0;
-        for (int k = 0; k <= maxkey; ++k) { off[k] = acc; acc += hist[k]; }
+        for (int k = 0; k <= maxkey; ++k) { pre[k] = acc; acc += hist[k]; }
     }
     __syncthreads();
-    for (int i = tid; i < B; i += blockDim.x) perm[atomicAdd(&off[maxkey - min(max(nit[i], 0), maxkey)], 1)] = i;
+    const int i = blockIdx.x * blockDim.x + tid;
+    int key = 0, pos = 0;
+    if (i < B) {
+        key = iters_key(nit[i], maxkey);
+        pos = atomicAdd(&lcount[key], 1);
+    }
+    __syncthreads();
+    if (tid <= maxkey && lcount[tid] > 0) lbase[tid] = pre[tid] + atomicAdd(&run[tid], lcount[tid]);
+    __syncthreads();
+    if (i < B) perm[lbase[key] + pos] = i;
+    if (blockIdx.x == 0 && tid < 64) {
+        whist[(1 - q) * 64 + tid] = 0;
+        whist[128 + (1 - q) * 64 + tid] = 0;
+    }
 }
 
 __global__ void iota_kernel(int B, int32_t* perm) {
@@ -1455,27 +1478,31 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
-    const bool sorted = a.wperm && a.wnit && a.p.qp_iters < 64;
+    const bool sorted = a.wperm && a.wnit && a.whist && a.p.qp_iters < 64;
+    SolveArgs as = a;
+    if (!sorted) as.whist = nullptr;
     if (e == hipSuccess && sorted) {
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemsetAsync(a.whist, 0, 4 * 64 * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
     const size_t tot = (size_t)a.B * (a.p.N + 1);
     const unsigned gl = (unsigned)((tot + 255) / 256);
     for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
         if (sorted && it > 0) {
-            hipLaunchKernelGGL(sort_by_iters_kernel, dim3(1), dim3(1024), 0, stream, a.B, a.p.qp_iters, a.wnit, a.wperm);
+            hipLaunchKernelGGL(sort_by_iters_kernel, dim3((a.B + 255) / 256), dim3(256), 0, stream, a.B, a.p.qp_iters,
+                               a.wnit, a.wperm, a.whist, (it - 1) & 1);
             e = hipGetLastError();
             if (e != hipSuccess) break;
         }
         const bool merit = a.p.nlp_mode == 1;
         if (merit) {   // the line search reads the stage data too: linearise into the workspace
-            hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, a);
+            hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, as);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = mark();
-        if (e == hipSuccess) e = merit ? launch_sqp_merit(a, it, stream) : launch_qp_any(a, S, it, stream, true);
+        if (e == hipSuccess) e = merit ? launch_sqp_merit(as, it, stream) : launch_qp_any(as, S, it, stream, true);
         if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;
