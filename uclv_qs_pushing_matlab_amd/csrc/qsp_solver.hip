@@ -38,34 +38,78 @@
 namespace qsp {
 
 // ------------------------------------------------------------- group helpers
-// Reductions over the L lanes of an instance group: a log-step tree towards the
-// group's first lane, then a broadcast, so every lane of the group holds the same
-// value (identical decisions in all lanes of an instance).
-__device__ __forceinline__ double group_sum(double v, int base, int L) {
-    const int lig = (int)(threadIdx.x & 63) - base;
-    for (int off = 1; off < L; off <<= 1) {
-        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
-        v += (lig + off < L) ? o : 0.0;
-    }
-    return __shfl(v, base);
-}
-__device__ __forceinline__ double group_min(double v, int base, int L) {
-    const int lig = (int)(threadIdx.x & 63) - base;
-    for (int off = 1; off < L; off <<= 1) {
-        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
-        v = (lig + off < L) ? fmin(v, o) : v;
-    }
-    return __shfl(v, base);
+// Reductions over the L lanes of an instance group (lanes base .. base+L-1), leaving the
+// same value in every lane of the group (identical decisions in all lanes of an instance).
+// Minima and maxima: a segmented inclusive scan over the whole wave with DPP row shifts
+// (1, 2, 4, 8 inside each row of 16) and the row broadcasts of lanes 15 and 31 —
+// register-to-register moves on the VALU, no LDS round trip — gathers the group's value in
+// its last lane; one shuffle broadcasts it.  A lane takes a shifted value only when its
+// source lane lies in the same group, so groups of any length L <= 64 and any alignment
+// reduce independently.  Sums: see group_sum.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_move(double v) {
+    // lanes without a source (row edge, rows outside ROWS) read 0, which the caller's group
+    // mask never takes.  (update_dpp, not mov_dpp: the move must stay outside the masked
+    // select — a DPP read from a lane disabled by EXEC does not return that lane's value.)
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xf, false);
+    return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double group_max(double v, int base, int L) {
-    const int lig = (int)(threadIdx.x & 63) - base;
-    for (int off = 1; off < L; off <<= 1) {
-        const double o = __shfl(v, (int)(threadIdx.x & 63) + off);
-        v = (lig + off < L) ? fmax(v, o) : v;
+// Which scan steps a lane takes (its source lane lies in the same group); computed once.
+struct GroupScan {
+    bool s1, s2, s4, s8, b15, b31;
+    int last;   // the group's last lane, where the scan completes
+    int base, L;
+    __device__ void init(int base_, int L_) {
+        base = base_;
+        L = L_;
+        const int lane = (int)(threadIdx.x & 63);
+        const int lig = lane - base_, col = lane & 15, row = lane >> 4;
+        s1 = col >= 1 && lig >= 1;
+        s2 = col >= 2 && lig >= 2;
+        s4 = col >= 4 && lig >= 4;
+        s8 = col >= 8 && lig >= 8;
+        b15 = (row & 1) && lig > col;          // row_bcast:15 into rows 1, 3 (source 16 row - 1)
+        b31 = row >= 2 && lig >= lane - 31;    // row_bcast:31 into rows 2, 3 (source 31)
+        last = base_ + L_ - 1;
     }
-    return __shfl(v, base);
+};
+
+// op(v, take ? o : identity) as a select on the moved value (never a branch: the DPP move
+// must execute with every lane enabled)
+struct OpMin {
+    __device__ double operator()(double v, double o, bool take) const { return (take && o < v) ? o : v; }
+};
+struct OpMax {
+    __device__ double operator()(double v, double o, bool take) const { return (take && o > v) ? o : v; }
+};
+
+template <class Op>
+__device__ __forceinline__ double group_reduce(double v, const GroupScan& g, Op op) {
+    v = op(v, dpp_move<0x111, 0xf>(v), g.s1);    // row_shr:1
+    v = op(v, dpp_move<0x112, 0xf>(v), g.s2);    // row_shr:2
+    v = op(v, dpp_move<0x114, 0xf>(v), g.s4);    // row_shr:4
+    v = op(v, dpp_move<0x118, 0xf>(v), g.s8);    // row_shr:8
+    v = op(v, dpp_move<0x142, 0xa>(v), g.b15);   // row_bcast:15
+    v = op(v, dpp_move<0x143, 0xc>(v), g.b31);   // row_bcast:31
+    return __shfl(v, g.last);
 }
+// Sums keep a log-step shuffle tree towards the group's first lane: its association depends
+// only on the lane's place in the group, so an instance's result does not depend on where
+// the wave packing puts it (a row-aligned scan would round differently at another offset;
+// min and max are exact in any order).
+__device__ __forceinline__ double group_sum(double v, const GroupScan& g) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int lig = lane - g.base;
+    for (int off = 1; off < g.L; off <<= 1) {
+        const double o = __shfl(v, lane + off);
+        v += (lig + off < g.L) ? o : 0.0;
+    }
+    return __shfl(v, g.base);
+}
+__device__ __forceinline__ double group_min(double v, const GroupScan& g) { return group_reduce(v, g, OpMin()); }
+__device__ __forceinline__ double group_max(double v, const GroupScan& g) { return group_reduce(v, g, OpMax()); }
 
 // 1/x from the hardware reciprocal refined by two Newton steps (≈ 5 instructions
 // instead of the ≈ 10 of the IEEE division sequence); for the positive, finite
@@ -130,6 +174,7 @@ struct Ctx {
     int lane, L, grp, lig, base, N;
     bool real;
     int inst;
+    GroupScan gs;
 };
 
 template <int S>
@@ -510,7 +555,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
             st.f(F_VN, ls, q) = 0.0;
         }
     }
-    r0 = group_max(r0, c.base, c.L);
+    r0 = group_max(r0, c.gs);
     double rscale = 1.0;
     int nit = 0;
     for (int it = 0; it < p.qp_iters; ++it) {
@@ -519,7 +564,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int ls = 0; ls < S; ++ls)
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
-        const double mu = group_sum(tl_sum, c.base, c.L) / m;
+        const double mu = group_sum(tl_sum, c.gs) / m;
         // stop on complementarity AND bound feasibility (as HPIPM checks both)
         const bool done = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop));
         if (__ballot(!done) == 0ull) break;
@@ -531,12 +576,12 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         double num = 1.0, den = 1.0, dummy = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, dummy, 0.0, false, 0.0);
-        const double aa = group_min(num / den, c.base, c.L);
+        const double aa = group_min(num / den, c.gs);
         double ma = 0.0;
         num = 1.0; den = 1.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, ma, aa, false, 0.0);
-        const double mua = group_sum(ma, c.base, c.L) / m;
+        const double mua = group_sum(ma, c.gs) / m;
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
         const double smu = sg * mu;
@@ -547,7 +592,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, false, 0.0);
-        double alpha = p.frac * group_min(num / den, c.base, c.L);
+        double alpha = p.frac * group_min(num / den, c.gs);
         alpha = fmin(alpha, 1.0);
         if (done) alpha = 0.0;
         rscale *= 1.0 - alpha;
@@ -867,10 +912,10 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
 #pragma unroll
         for (int i = 0; i < 4; ++i) rs = fmax(rs, fabs(st.g[0][i] - PIp[i]));
     }
-    rs = group_max(rs, c.base, c.L);
-    re = group_max(re, c.base, c.L);
-    ri = group_max(ri, c.base, c.L);
-    rc = group_max(rc, c.base, c.L);
+    rs = group_max(rs, c.gs);
+    re = group_max(re, c.gs);
+    ri = group_max(ri, c.gs);
+    rc = group_max(rc, c.gs);
     return rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
 }
 
@@ -886,6 +931,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     c.grp = c.lane / c.L;
     c.lig = c.lane - c.grp * c.L;
     c.base = c.grp * c.L;
+    c.gs.init(c.base, c.L);
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
     c.real = (c.grp < G) && (c.inst < A.B);
@@ -986,7 +1032,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
             bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
         }
-        failed = !skip && group_max(bad, c.base, c.L) > 0.0;
+        failed = !skip && group_max(bad, c.gs) > 0.0;
         if (failed && c.real && c.lig == 0) {
             A.wdone[iv] = 2;
             A.sqp_iter[iv] = it;
@@ -1113,6 +1159,7 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
     c.grp = c.lane / c.L;
     c.lig = c.lane - c.grp * c.L;
     c.base = c.grp * c.L;
+    c.gs.init(c.base, c.L);
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
     c.real = (c.grp < G) && (c.inst < A.B);
@@ -1176,8 +1223,8 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
             if (hi < 0.0) dph -= ETAk[2 * j + 1] * (-hi);
         }
     }
-    const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, bb, NUk, ETAk), c.base, c.L);
-    const double dphi = group_sum(dph, c.base, c.L);
+    const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, bb, NUk, ETAk), c.gs);
+    const double dphi = group_sum(dph, c.gs);
     double alpha = 1.0;
     bool fin = skip;
     while (__ballot(!fin) != 0ull) {
@@ -1197,7 +1244,7 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) def[q] = 0.0;
         }
-        const double phi = group_sum(merit_stage(p, k, xt, ut, yr, ye, def, NUk, ETAk), c.base, c.L);
+        const double phi = group_sum(merit_stage(p, k, xt, ut, yr, ye, def, NUk, ETAk), c.gs);
         if (!fin) {
             if (phi <= phi0 + p.ls_eps * alpha * dphi) {
                 fin = true;
