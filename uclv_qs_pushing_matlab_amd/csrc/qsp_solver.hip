@@ -749,46 +749,6 @@ __global__ void prologue_kernel(SolveArgs A) {
     }
 }
 
-// Stage-parallel linearisation: one thread per (instance, stage k = 0..N).
-__global__ void __launch_bounds__(256) linearize_kernel(SolveArgs A) {
-    const SolveParams& p = A.p;
-    const int N = p.N;
-    const size_t tot = (size_t)A.B * (N + 1);
-    const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gi >= tot) return;
-    const int i = (int)(gi / (N + 1)), k = (int)(gi - (size_t)i * (N + 1));
-    if (A.wdone && A.wdone[i]) return;                                      // frozen instance
-    const ShapeDev& sh = shape_of(A, i);
-    const double* X = A.wX + (size_t)i * (N + 1) * 4;
-    double* out = A.wlin + gi;
-    if (k < N) {
-        const double xk[4] = {X[4 * k], X[4 * k + 1], X[4 * k + 2], X[4 * k + 3]};
-        const double uk[2] = {A.wU[((size_t)i * N + k) * 2], A.wU[((size_t)i * N + k) * 2 + 1]};
-        Lin L;
-        rk4<true>(sh, p.Ts, xk, uk, L);
-        const double* yr = A.yref + ((size_t)i * N + k) * 6;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) out[(L_A + q) * tot] = L.a[q];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) out[(L_B + q) * tot] = L.B[q];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) out[(L_BB + q) * tot] = L.xn[q] - X[4 * (k + 1) + q];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) out[(L_G + q) * tot] = p.tau * p.W[q] * (xk[q] - yr[q]);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) out[(L_G + 4 + q) * tot] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
-    } else {
-        // terminal stage: no dynamics (the QP never reads A, B, b here; defined anyway)
-#pragma unroll
-        for (int q = 0; q < L_G; ++q) out[q * tot] = 0.0;
-        const double* ye = A.yref_e + (size_t)i * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) out[(L_G + q) * tot] = p.We[q] * (X[4 * N + q] - ye[q]);
-        out[(L_G + 4) * tot] = 0.0;
-        out[(L_G + 5) * tot] = 0.0;
-    }
-}
-
 // The QP of one SQP iteration in the register/LDS-resident lane-group layout:
 // load stage data, Mehrotra IPM, roll out the damped step, update the SQP iterate.
 // Dynamics multipliers of the QP solution, one per stage lane (S = 1): lane k < N
@@ -948,15 +908,18 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     }
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
+    // frozen instances (converged in nlp_mode 1, or a failed QP earlier) are not iterated
+    const bool was_done = A.wdone && A.wdone[iv] != 0;
+    const bool lin_live = c.real && !was_done;   // fused linearisation only where it is used
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
         const int kc = k <= N ? k : N;
         const int ku = k < N ? k : N - 1;
         if constexpr (LIN) {
-            // fused linearisation (linearize_kernel's arithmetic, one stage per slot): the
+            // the SQP iteration's linearisation, one stage per slot (RK4 + sensitivities): the
             // stage data stays in registers instead of a 24-double HBM round trip
-            if (kc < N) {
+            if (kc < N && lin_live) {
                 const double xk[4] = {X[4 * kc], X[4 * kc + 1], X[4 * kc + 2], X[4 * kc + 3]};
                 const double uk[2] = {U[2 * kc], U[2 * kc + 1]};
                 Lin Ln;
@@ -972,7 +935,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
                 for (int q = 0; q < 4; ++q) st.g[ls][q] = p.tau * p.W[q] * (xk[q] - yr[q]);
 #pragma unroll
                 for (int q = 0; q < 2; ++q) st.g[ls][4 + q] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
-            } else {
+            } else {   // terminal stage (or an instance that does not iterate): no dynamics
                 const double* ye = A.yref_e + (size_t)iv * 4;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) st.a[ls][q] = 0.0;
@@ -1000,11 +963,19 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         st.v(ls, 1) = U[2 * ku];
         st.v(ls, 2) = U[2 * ku + 1];
     }
+    if constexpr (MERIT && LIN) {
+        // the line search (merit_ls_kernel) evaluates the defect and gradient at the same point
+        if (lin_live && c.lig <= N) {
+            double* out = A.wlin + (size_t)iv * (N + 1) + c.lig;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[(L_BB + q) * tot] = st.bb[0][q];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) out[(L_G + q) * tot] = st.g[0][q];
+        }
+    }
     double dx0[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];   // used by lane lig == 0
-    // frozen instances (converged in nlp_mode 1, or a failed QP earlier) are not iterated
-    const bool was_done = A.wdone && A.wdone[iv] != 0;
     // padding lanes (no instance) must not hold their wave in the IPM loop: they mirror
     // instance B-1 with group reductions over foreign lanes and need not converge
     bool skip = was_done || !c.real;
@@ -1506,11 +1477,11 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)qp_step_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  lds_bytes<1>());
+        (void)hipFuncSetAttribute((const void*)qp_step_kernel<1, true, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<1>());
         attr = true;
     }
-    hipLaunchKernelGGL((qp_step_kernel<1, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(merit_ls_kernel, dim3((waves * 64 + 255) / 256), dim3(256), 0, stream, a);
@@ -1534,8 +1505,6 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
         if (e == hipSuccess) e = hipMemsetAsync(a.whist, 0, 4 * 64 * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
-    const size_t tot = (size_t)a.B * (a.p.N + 1);
-    const unsigned gl = (unsigned)((tot + 255) / 256);
     for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
         if (sorted && it > 0) {
             hipLaunchKernelGGL(sort_by_iters_kernel, dim3((a.B + 255) / 256), dim3(256), 0, stream, a.B, a.p.qp_iters,
@@ -1544,10 +1513,6 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
             if (e != hipSuccess) break;
         }
         const bool merit = a.p.nlp_mode == 1;
-        if (merit) {   // the line search reads the stage data too: linearise into the workspace
-            hipLaunchKernelGGL(linearize_kernel, dim3(gl), dim3(256), 0, stream, as);
-            e = hipGetLastError();
-        }
         if (e == hipSuccess) e = mark();
         if (e == hipSuccess) e = merit ? launch_sqp_merit(as, it, stream) : launch_qp_any(as, S, it, stream, true);
         if (e == hipSuccess) e = mark();
