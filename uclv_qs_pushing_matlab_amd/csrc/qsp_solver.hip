@@ -205,6 +205,13 @@ __device__ __forceinline__ double wave_from_next(double old, double v) {
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x130, 0xf, 0xf, false);
     return __hiloint2double(hi, lo);
 }
+// lane i <- lane i-1's v; lane 0 keeps `old` (the walks never read it there), so the
+// result can take old's register in a loop without a copy
+__device__ __forceinline__ double wave_from_prev(double old, double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_from_prev(double v) {   // lane i <- lane i-1
     const int l = __double2loint(v), h = __double2hiint(v);
     const int lo = __builtin_amdgcn_update_dpp(l, l, 0x138, 0xf, 0xf, false);
@@ -425,7 +432,7 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
 // (F_VA / F_VN).
 template <int S, bool FACTOR>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
-                                              int out) {
+                                              int out, double (&M)[S][16]) {
     double P[10], pv[4];
 #pragma unroll
     for (int i = 0; i < 10; ++i) P[i] = 0.0;
@@ -495,6 +502,47 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 #pragma unroll
             for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
         }
+    }
+    if constexpr (S == 1) {
+        // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
+        // one 4x4 affine map (16 FMA) instead of du = kk + K dx followed by the dynamics;
+        // each lane keeps the dx of its own turn and forms du = kk + K dx afterwards, in
+        // parallel.  A + B K is built once per factorisation (the corrector reuses it).
+        if (FACTOR) {
+            const double* a = st.a[0];
+            const double* B = st.B[0];
+            const double* K = st.K[0];
+            const double Am[4][4] = {{1.0, 0.0, a[0], a[1]}, {0.0, 1.0, a[2], a[3]}, {0.0, 0.0, 1.0, a[4]},
+                                     {0.0, 0.0, 0.0, a[5]}};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) M[0][4 * i + q] = Am[i][q] + B[2 * i] * K[q] + B[2 * i + 1] * K[4 + q];
+        }
+        double cv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cv[i] = st.bb[0][i] + st.B[0][2 * i] * st.kk[0][0] + st.B[0][2 * i + 1] * st.kk[0][1];
+        double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
+        double dxk[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < c.L - 1; ++j) {
+            if (c.lig == j) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dxk[i] = dx[i];
+            }
+            double n[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                n[i] = cv[i] + M[0][4 * i] * dx[0] + M[0][4 * i + 1] * dx[1] + M[0][4 * i + 2] * dx[2] + M[0][4 * i + 3] * dx[3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i], n[i]);
+        }
+        if (c.lig < c.N) {
+            const double* K = st.K[0];
+            st.f(out, 0, 0) = dxk[3];
+            st.f(out, 0, 1) = st.kk[0][0] + K[0] * dxk[0] + K[1] * dxk[1] + K[2] * dxk[2] + K[3] * dxk[3];
+            st.f(out, 0, 2) = st.kk[0][1] + K[4] * dxk[0] + K[5] * dxk[1] + K[6] * dxk[2] + K[7] * dxk[3];
+        }
+        return;
     }
     // forward: every slot of lanes 0 .. L-2 is a stage k < N; the last lane holds lsN of them
     double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
@@ -572,7 +620,8 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         // ---- predictor
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S, false>(c, p, st, ls, 0.0);
-        riccati_solve<S, true>(c, p, st, dx0, F_VA);
+        double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
+        riccati_solve<S, true>(c, p, st, dx0, F_VA, M);
         double num = 1.0, den = 1.0, dummy = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, dummy, 0.0, false, 0.0);
@@ -588,7 +637,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         // ---- corrector
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S, true>(c, p, st, ls, smu);
-        riccati_solve<S, false>(c, p, st, dx0, F_VN);
+        riccati_solve<S, false>(c, p, st, dx0, F_VN, M);
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, false, 0.0);
