@@ -466,6 +466,39 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             gu[ls][1] = st.hg(ls, 5);
         }
     }
+    if constexpr (S == 1 && !FACTOR) {
+        // corrector difference walk in closed-loop form: dp_k = e_k + (A + B K)' dp_{k+1} with
+        // e = dg_x + K' dg_u (ric_delta_step with dr = dg_u + B' dp substituted), a 4x4 map per
+        // step; each lane keeps the dp that reaches it and forms dkk = Rn (dg_u + B' dp)
+        // afterwards, in parallel
+        const double* K = st.K[0];
+        double e[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e[i] = (i == 3 ? gx3[0] : 0.0) + K[i] * gu[0][0] + K[4 + i] * gu[0][1];
+        double dpk[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = c.L - 2; j >= 0; --j) {
+            if (c.lig == j) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dpk[i] = pv[i];
+            }
+            double n[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                n[i] = e[i] + M[0][i] * pv[0] + M[0][4 + i] * pv[1] + M[0][8 + i] * pv[2] + M[0][12 + i] * pv[3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], n[i]);
+        }
+        if (c.lig < c.N) {
+            const double* B = st.B[0];
+            const double* Rn = st.Rn[0];
+            double rt[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                rt[i] = gu[0][i] + B[i] * dpk[0] + B[2 + i] * dpk[1] + B[4 + i] * dpk[2] + B[6 + i] * dpk[3];
+            st.kk[0][0] += Rn[0] * rt[0] + Rn[1] * rt[1];
+            st.kk[0][1] += Rn[1] * rt[0] + Rn[2] * rt[1];
+        }
+    } else
     for (int j = c.L - 1; j >= 0; --j) {
         // Lanes above j already hold their final factors and sit the step out (exec
         // mask); lanes below j compute a throw-away step that their own turn overwrites.
