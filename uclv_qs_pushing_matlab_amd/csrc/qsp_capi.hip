@@ -104,12 +104,11 @@ static void fill_params(qsp_solver* s) {
 }
 
 static int auto_S(int N) {
-    // Instances per wavefront G(S) = 64 / ceil((N+1)/S).  One stage per lane keeps the
-    // kernel at 2 waves/SIMD and wins while two stages per lane do not at least double G
-    // (profiles/r01: N = 20 S = 1 239k vs S = 2 224k solves/s; N = 50 S = 2 is 1.32x S = 1).
-    const int g1 = N + 1 <= 64 ? 64 / (N + 1) : 0;
-    const int g2 = 64 / ((N + 2) / 2);
-    return (g1 > 0 && g2 < 2 * g1) ? 1 : 2;
+    // One stage per lane keeps the QP kernel at 2 waves/SIMD with its closed-loop walks;
+    // two stages per lane spill into AGPRs at 1 wave/SIMD and lose at every measured
+    // horizon (scripts/layout_sweep.sh, round 1: N = 10 1.21M vs 1.02M, N = 20 428k vs 325k,
+    // N = 50 (B = 16 384) 55.1k vs 54.2k solves/s).  S = 2 remains for N + 1 > 64.
+    return N + 1 <= 64 ? 1 : 2;
 }
 
 // Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
