@@ -8,19 +8,22 @@
 // IPM iterations.  Stage-parallel work (barrier terms, step lengths) runs on all
 // lanes at once; the horizon recursions (Riccati backward, state forward, adjoint)
 // walk the group lane by lane, handing the 4x4 value function / state step to the
-// neighbour lane with one DPP wave shift.
+// neighbour lane with one DPP wave shift.  With one stage per lane the walks after the
+// factorisation run in closed-loop form (one 4x4 affine map per step).
 //
-// One solve = prologue (NMPC_controller.solve wrapper) + K x (linearize [RK4 +
-// sensitivities, one thread per stage], qp_step [one QP per instance]) + epilogue.
+// One solve = prologue (NMPC_controller.solve wrapper) + K x qp_step [linearisation
+// (RK4 + sensitivities, one lane per stage) and one QP per instance] + epilogue.
 // Before each QP launch the instances are packed into waves by the IPM iteration
-// count of their previous QP, longest first (sort_by_iters_kernel).
+// count of their previous QP, longest first (sort_by_iters_kernel, on a histogram the
+// QP kernel accumulates).
 //
 // Algorithm (restating the reference OCP, NMPC_controller.m:174-300):
 //   SQP  : nlp_mode 0 — fixed-K full Gauss-Newton steps (BASELINE "SQP-RTI, K iterations");
 //          nlp_mode 1 — the reference's 'SQP' + 'merit_backtracking': KKT test with
 //          tol 1e-6, l1-merit Armijo backtracking (qp_step<1, true> + merit_ls_kernel)
 //   QP   : box-constrained LQ-OCP, Mehrotra predictor-corrector interior point,
-//          Riccati factorisation reused by the corrector (stands in for HPIPM);
+//          Riccati factorisation reused by the corrector, whose backward pass runs
+//          on the difference to the predictor (stands in for HPIPM);
 //          stops on mu < mu_stop and bound residual < res_stop, or at qp_iters
 //   model: RK4 (1 step, h = Ts) + forward sensitivities of f (qsp_math.hpp)
 // Also here: the device closed loop (plant_kernel, helper.m:195-322), per-lane
