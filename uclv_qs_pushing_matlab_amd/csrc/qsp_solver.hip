@@ -1232,8 +1232,10 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
     const ShapeDev& sh = shape_of(A, iv);
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
-    double xk[4], uk[2], dxk[4], duk[2], piq[4], lamq[6], bb[4], g[6];
-    double PIk[4], LAMk[6], NUk[4], ETAk[6];
+    // what the backtracking loop reads stays in registers; the multipliers are read again
+    // for the update after it (fewer live registers: more waves per SIMD)
+    double xk[4], uk[2], dxk[4], duk[2], bb[4], g[6];
+    double NUk[4], ETAk[6];
 #pragma unroll
     for (int q = 0; q < 4; ++q) xk[q] = X[4 * k + q];
     uk[0] = U[2 * ku];
@@ -1242,24 +1244,28 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
     const double* in = A.wlin + si;
     const double* nl = A.wnlp + si;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { dxk[q] = skip ? 0.0 : w[(Q_DX + q) * tot]; piq[q] = skip ? 0.0 : w[(Q_PI + q) * tot]; }
+    for (int q = 0; q < 4; ++q) dxk[q] = skip ? 0.0 : w[(Q_DX + q) * tot];
 #pragma unroll
     for (int q = 0; q < 2; ++q) duk[q] = (skip || !stg) ? 0.0 : w[(Q_DU + q) * tot];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) lamq[q] = (skip || !stg) ? 0.0 : w[(Q_LAM + q) * tot];
 #pragma unroll
     for (int q = 0; q < 4; ++q) bb[q] = in[(L_BB + q) * tot];
 #pragma unroll
     for (int q = 0; q < 6; ++q) g[q] = in[(L_G + q) * tot];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { PIk[q] = nl[(W_PI + q) * tot]; NUk[q] = nl[(W_NU + q) * tot]; }
+    for (int q = 0; q < 4; ++q) NUk[q] = nl[(W_NU + q) * tot];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) { LAMk[q] = nl[(W_LAM + q) * tot]; ETAk[q] = nl[(W_ETA + q) * tot]; }
+    for (int q = 0; q < 6; ++q) ETAk[q] = nl[(W_ETA + q) * tot];
     if (stg) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { const double a = fabs(piq[q]), wq = 0.5 * (NUk[q] + a); NUk[q] = a > wq ? a : wq; }
+        for (int q = 0; q < 4; ++q) {
+            const double a = skip ? 0.0 : fabs(w[(Q_PI + q) * tot]), wq = 0.5 * (NUk[q] + a);
+            NUk[q] = a > wq ? a : wq;
+        }
 #pragma unroll
-        for (int q = 0; q < 6; ++q) { const double a = fabs(lamq[q]), wq = 0.5 * (ETAk[q] + a); ETAk[q] = a > wq ? a : wq; }
+        for (int q = 0; q < 6; ++q) {
+            const double a = skip ? 0.0 : fabs(w[(Q_LAM + q) * tot]), wq = 0.5 * (ETAk[q] + a);
+            ETAk[q] = a > wq ? a : wq;
+        }
     }
     const double* yr = A.yref + ((size_t)iv * N + ku) * 6;
     const double* ye = A.yref_e + (size_t)iv * 4;
@@ -1319,9 +1325,15 @@ __global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
         U[2 * k + 1] = uk[1] + alpha * duk[1];
         double* nw = A.wnlp + si;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) nw[(W_PI + q) * tot] = PIk[q] + alpha * (piq[q] - PIk[q]);
+        for (int q = 0; q < 4; ++q) {
+            const double pk = nw[(W_PI + q) * tot];
+            nw[(W_PI + q) * tot] = pk + alpha * (w[(Q_PI + q) * tot] - pk);
+        }
 #pragma unroll
-        for (int q = 0; q < 6; ++q) nw[(W_LAM + q) * tot] = LAMk[q] + alpha * (lamq[q] - LAMk[q]);
+        for (int q = 0; q < 6; ++q) {
+            const double lk = nw[(W_LAM + q) * tot];
+            nw[(W_LAM + q) * tot] = lk + alpha * (w[(Q_LAM + q) * tot] - lk);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) nw[(W_NU + q) * tot] = NUk[q];
 #pragma unroll
