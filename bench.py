@@ -278,9 +278,12 @@ def main():
         # a lane is 'stable' when the oracle itself stays put (< 1e-9) under three 1e-13 relative
         # perturbations of x0: the full-step SQP amplifies rounding on the other lanes
         stable = np.ones(m, bool)
+        self_dev = np.zeros(m)   # how far the oracle itself moves under the perturbations
         for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
             rp = run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13))
-            stable &= np.abs(rp["u0"] - u0_ref[:m]).max(1) < 1e-9
+            dev = np.abs(rp["u0"] - u0_ref[:m]).max(1)
+            stable &= dev < 1e-9
+            self_dev = np.maximum(self_dev, dev)
         # ... and converged (the K-1 and K iterates agree: not a limit cycle of the full-step SQP)
         if args.nlp == "SQP_RTI":
             stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
@@ -292,6 +295,11 @@ def main():
                             "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
                             "stable_lanes": int(stable.sum()), "stable_checked": int(m),
                             "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
+                            # the same statistic for the oracle against itself under 1e-13 relative
+                            # perturbations of x0 (first `stable_checked` lanes): the GPU/oracle gap
+                            # on the remaining lanes is the problem's own sensitivity
+                            "frac_lanes_err_le_1e-6_first": float(np.mean(d[:m] <= 1e-6)),
+                            "oracle_self_frac_le_1e-6_first": float(np.mean(self_dev <= 1e-6)),
                             "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
                                     "< 1e-9 under three 1e-13 relative perturbations of x0, between K-1 and K "
                                     "iterations and with mu_stop 1.5e-10 (converged, non-chaotic lane)"}
