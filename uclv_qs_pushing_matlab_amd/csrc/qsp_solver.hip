@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "qsp_math.hpp"
 #include "qsp_kernels.h"
 
@@ -1539,6 +1541,19 @@ __global__ void vbound_kernel(const ShapeDev* shapes, const int32_t* sid, int n,
 }
 
 // ------------------------------------------------------------------ launchers
+// The QP kernels take more than 64 KB of dynamic LDS, which a kernel must be allowed once per
+// device (one bit per device in `done`; handles on several devices may share a process).
+static hipError_t lds_attr_once(const void* kernel, int bytes, std::atomic<uint64_t>& done) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
+
 // LIN: the SQP iteration's linearisation runs inside the QP kernel (nlp_mode 0); without
 // it the kernel reads the stage data the workspace holds (qsp_qp_solve).
 template <int S, bool LIN>
@@ -1547,12 +1562,9 @@ static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream)
     const int G = 64 / L;
     const int waves = (a.B + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)qp_step_kernel<S, false, LIN>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<S>());
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN>, lds_bytes<S>(), attr);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((qp_step_kernel<S, false, LIN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
     return hipGetLastError();
 }
@@ -1572,12 +1584,9 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     const int G = 64 / L;
     const int waves = (a.B + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)qp_step_kernel<1, true, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<1>());
-        attr = true;
-    }
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t ea = lds_attr_once((const void*)qp_step_kernel<1, true, true>, lds_bytes<1>(), attr);
+    if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
