@@ -480,19 +480,20 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         double e[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) e[i] = (i == 3 ? gx3[0] : 0.0) + K[i] * gu[0][0] + K[4 + i] * gu[0][1];
-        double dpk[4] = {0.0, 0.0, 0.0, 0.0};
+        // Step j runs on lanes lig <= j only: lane j-1 takes lane j's value, while lane j,
+        // whose source lane j+1 sits the step out, keeps its old value (a DPP read from a
+        // disabled lane returns `old`) — so every lane ends holding the dp that reached it.
         for (int j = c.L - 2; j >= 0; --j) {
-            if (c.lig == j) {
+            if (c.lig <= j) {
+                double n[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) dpk[i] = pv[i];
+                for (int i = 0; i < 4; ++i)
+                    n[i] = e[i] + M[0][i] * pv[0] + M[0][4 + i] * pv[1] + M[0][8 + i] * pv[2] + M[0][12 + i] * pv[3];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], n[i]);
             }
-            double n[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                n[i] = e[i] + M[0][i] * pv[0] + M[0][4 + i] * pv[1] + M[0][8 + i] * pv[2] + M[0][12 + i] * pv[3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], n[i]);
         }
+        const double* dpk = pv;
         if (c.lig < c.N) {
             const double* B = st.B[0];
             const double* Rn = st.Rn[0];
@@ -544,7 +545,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
     if constexpr (S == 1) {
         // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
         // one 4x4 affine map (16 FMA) instead of du = kk + K dx followed by the dynamics;
-        // each lane keeps the dx of its own turn and forms du = kk + K dx afterwards, in
+        // each lane keeps the dx of its own stage and forms du = kk + K dx afterwards, in
         // parallel.  A + B K is built once per factorisation (the corrector reuses it).
         if (FACTOR) {
             const double* a = st.a[0];
@@ -561,19 +562,21 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 #pragma unroll
         for (int i = 0; i < 4; ++i) cv[i] = st.bb[0][i] + st.B[0][2 * i] * st.kk[0][0] + st.B[0][2 * i + 1] * st.kk[0][1];
         double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
-        double dxk[4] = {0.0, 0.0, 0.0, 0.0};
+        // Step j runs on lanes j <= lig < L-1 only (the terminal lane never steps, so the
+        // next group's first lane reads a disabled source): lane j+1 takes lane j's value and
+        // lane j keeps its own, so every lane ends holding the dx of its stage.
         for (int j = 0; j < c.L - 1; ++j) {
-            if (c.lig == j) {
+            if (c.lig >= j && c.lig < c.L - 1) {
+                double n[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) dxk[i] = dx[i];
+                for (int i = 0; i < 4; ++i)
+                    n[i] = cv[i] + M[0][4 * i] * dx[0] + M[0][4 * i + 1] * dx[1] + M[0][4 * i + 2] * dx[2] +
+                           M[0][4 * i + 3] * dx[3];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i], n[i]);
             }
-            double n[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                n[i] = cv[i] + M[0][4 * i] * dx[0] + M[0][4 * i + 1] * dx[1] + M[0][4 * i + 2] * dx[2] + M[0][4 * i + 3] * dx[3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i], n[i]);
         }
+        const double* dxk = dx;
         if (c.lig < c.N) {
             const double* K = st.K[0];
             st.f(out, 0, 0) = dxk[3];
