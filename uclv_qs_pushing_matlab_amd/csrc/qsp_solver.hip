@@ -353,43 +353,95 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 }
 
 // ------------------------------------------------------------------ QP core
-// Barrier terms of slot ls into LDS: hg[0..2] Hessian additions, hg[3..5] gradient
-// additions.  Corrector: c_j = sigma_mu - dt_aff dl_aff (predictor: c_j = 0).
-template <int S, bool CORR>
-__device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls, double smu) {
+// Barrier terms of slot ls into LDS (predictor): hg[0..2] Hessian additions, hg[3..5]
+// gradient additions.  The corrector changes only the gradient (corrector_terms).
+template <int S>
+__device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls) {
     const int k = kof<S>(c, ls);
     double lo[3], hi[3];
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const bool act = (k < c.N) && (j > 0 || k >= 1);
-        const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
-        const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
-        const double sl = ll * rtl, sh = lh * rth;
-        if (CORR) {
-            // corrector: only the change of the gradient (ric_delta_step); the Hessian is the predictor's
-            const double v = st.f(F_VA, ls, j);
-            const double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
-            const double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
-            const double cl = smu - dtl * dll, ch = smu - dth * dlh;
-            st.hg(ls, 3 + j) = act ? ch * rth - cl * rtl : 0.0;
-        } else {
-            const double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
-            st.hg(ls, j) = act ? sl + sh : 0.0;
-            st.hg(ls, 3 + j) = act ? gadd : 0.0;
-        }
+        const double sl = ll * st.rt(ls, 2 * j), sh = lh * st.rt(ls, 2 * j + 1);
+        const double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
+        st.hg(ls, j) = act ? sl + sh : 0.0;
+        st.hg(ls, 3 + j) = act ? gadd : 0.0;
     }
 }
 
-// Slack/multiplier directions of slot ls from the bounded components of a QP
-// solution (field VSRC), folded into the step-length bound: the largest alpha with
-// t + alpha dt >= 0 and l + alpha dl >= 0 is tracked as a ratio num/den without
-// dividing (den > 0).  UPDATE: apply t += alpha dt, l += alpha dl instead.
-template <int S, bool CORR>
-__device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls, int vsrc,
-                                           double smu, double& num, double& den, double& mu_aff_part, double alpha_aff,
-                                           bool update, double alpha) {
+// The step length is the largest alpha with t + alpha dt >= 0 and l + alpha dl >= 0,
+// tracked as a ratio num/den without dividing (den > 0): a candidate t/(-dt) replaces
+// num/den when t * den < num * (-dt).
+// Affine (predictor) slack/multiplier directions of slot ls from its bounded QP solution
+// components (F_VA), unmasked, kept in registers for the rest of the IPM iteration:
+// at/al[2j] lower, [2j+1] upper bound of component j.  Also folds the masked directions
+// into the step-length ratio num/den.
+template <int S>
+__device__ __forceinline__ void affine_dirs(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
+                                            double at[6], double al[6], double& num, double& den) {
+    const int k = kof<S>(c, ls);
+    double lo[3], hi[3];
+    bnd_lohi<S>(p, st, ls, lo, hi);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
+        const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
+        const double sl = ll * st.rt(ls, 2 * j), sh = lh * st.rt(ls, 2 * j + 1);
+        const double v = st.f(F_VA, ls, j);
+        at[2 * j] = v - lo[j] - tl;
+        at[2 * j + 1] = hi[j] - v - th;
+        al[2 * j] = -ll - sl * at[2 * j];
+        al[2 * j + 1] = -lh - sh * at[2 * j + 1];
+        const double dtl = act ? at[2 * j] : 0.0, dth = act ? at[2 * j + 1] : 0.0;
+        const double dll = act ? al[2 * j] : 0.0, dlh = act ? al[2 * j + 1] : 0.0;
+        if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
+        if (dth < 0.0 && th * den < num * -dth) { num = th; den = -dth; }
+        if (dll < 0.0 && ll * den < num * -dll) { num = ll; den = -dll; }
+        if (dlh < 0.0 && lh * den < num * -dlh) { num = lh; den = -dlh; }
+    }
+}
+
+// Complementarity after the affine step aa (Mehrotra's mu_aff), from the cached directions.
+template <int S>
+__device__ __forceinline__ double affine_mu_part(const Ctx& c, const Stage<S>& st, int ls, const double at[6],
+                                                 const double al[6], double aa) {
+    const int k = kof<S>(c, ls);
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
+        const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
+        const double dtl = act ? at[2 * j] : 0.0, dth = act ? at[2 * j + 1] : 0.0;
+        const double dll = act ? al[2 * j] : 0.0, dlh = act ? al[2 * j + 1] : 0.0;
+        part += (tl + aa * dtl) * (ll + aa * dll) + (th + aa * dth) * (lh + aa * dlh);
+    }
+    return part;
+}
+
+// Corrector barrier gradient change of slot ls from the cached affine directions (the
+// Hessian is the predictor's): hg[3+j] = c_h / t_h - c_l / t_l, c = sigma mu - dt_aff dl_aff.
+template <int S>
+__device__ __forceinline__ void corrector_terms(const Ctx& c, const Stage<S>& st, int ls, const double at[6],
+                                                const double al[6], double smu) {
+    const int k = kof<S>(c, ls);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const double cl = smu - at[2 * j] * al[2 * j], ch = smu - at[2 * j + 1] * al[2 * j + 1];
+        st.hg(ls, 3 + j) = act ? ch * st.rt(ls, 2 * j + 1) - cl * st.rt(ls, 2 * j) : 0.0;
+    }
+}
+
+// Corrector directions of slot ls (masked) from its bounded QP solution components (F_VN) and
+// the cached affine directions; folded into the ratio num/den and kept for the update.
+template <int S>
+__device__ __forceinline__ void corrector_dirs(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
+                                               const double at[6], const double al[6], double smu, double dt[6],
+                                               double dl[6], double& num, double& den) {
     const int k = kof<S>(c, ls);
     double lo[3], hi[3];
     bnd_lohi<S>(p, st, ls, lo, hi);
@@ -400,35 +452,32 @@ __device__ __forceinline__ void directions(const Ctx& c, const SolveParams& p, c
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
         const double sl = ll * rtl, sh = lh * rth;
-        const double v = st.f(vsrc, ls, j);
+        const double v = st.f(F_VN, ls, j);
         double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
         double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
-        if (CORR) {
-            const double va = st.f(F_VA, ls, j);
-            const double atl = va - lo[j] - tl, ath = hi[j] - va - th;
-            const double all = -ll - sl * atl, alh = -lh - sh * ath;
-            dll += (smu - atl * all) * rtl;
-            dlh += (smu - ath * alh) * rth;
-        }
+        dll += (smu - at[2 * j] * al[2 * j]) * rtl;
+        dlh += (smu - at[2 * j + 1] * al[2 * j + 1]) * rth;
         dtl = act ? dtl : 0.0; dth = act ? dth : 0.0;
         dll = act ? dll : 0.0; dlh = act ? dlh : 0.0;
-        if (update) {
-            const double tln = tl + alpha * dtl, thn = th + alpha * dth;
-            st.t(ls, 2 * j) = tln;
-            st.t(ls, 2 * j + 1) = thn;
-            st.rt(ls, 2 * j) = rcp(tln);
-            st.rt(ls, 2 * j + 1) = rcp(thn);
-            st.lm(ls, 2 * j) = ll + alpha * dll;
-            st.lm(ls, 2 * j + 1) = lh + alpha * dlh;
-        } else {
-            // ratio test: candidate t/(-dt) replaces num/den when t * den < num * (-dt)
-            if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
-            if (dth < 0.0 && th * den < num * -dth) { num = th; den = -dth; }
-            if (dll < 0.0 && ll * den < num * -dll) { num = ll; den = -dll; }
-            if (dlh < 0.0 && lh * den < num * -dlh) { num = lh; den = -dlh; }
-            if (!CORR) mu_aff_part += (tl + alpha_aff * dtl) * (ll + alpha_aff * dll) +
-                                      (th + alpha_aff * dth) * (lh + alpha_aff * dlh);
-        }
+        if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
+        if (dth < 0.0 && th * den < num * -dth) { num = th; den = -dth; }
+        if (dll < 0.0 && ll * den < num * -dll) { num = ll; den = -dll; }
+        if (dlh < 0.0 && lh * den < num * -dlh) { num = lh; den = -dlh; }
+        dt[2 * j] = dtl; dt[2 * j + 1] = dth;
+        dl[2 * j] = dll; dl[2 * j + 1] = dlh;
+    }
+}
+
+// Step of slot ls: t += alpha dt (and its reciprocal), l += alpha dl.
+template <int S>
+__device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const double dt[6], const double dl[6],
+                                           double alpha) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const double tn = st.t(ls, q) + alpha * dt[q];
+        st.t(ls, q) = tn;
+        st.rt(ls, q) = rcp(tn);
+        st.lm(ls, q) = st.lm(ls, q) + alpha * dl[q];
     }
 }
 
@@ -660,39 +709,39 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         nit += done ? 0 : 1;
         // ---- predictor
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) barrier_terms<S, false>(c, p, st, ls, 0.0);
+        for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls);
         double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
         riccati_solve<S, true>(c, p, st, dx0, F_VA, M);
-        double num = 1.0, den = 1.0, dummy = 0.0;
+        // affine directions: computed once, kept in registers through the corrector
+        double at[S][6], al[S][6];
+        double num = 1.0, den = 1.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, dummy, 0.0, false, 0.0);
+        for (int ls = 0; ls < S; ++ls) affine_dirs<S>(c, p, st, ls, at[ls], al[ls], num, den);
         const double aa = group_min(num / den, c.gs);
         double ma = 0.0;
-        num = 1.0; den = 1.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) directions<S, false>(c, p, st, ls, F_VA, 0.0, num, den, ma, aa, false, 0.0);
+        for (int ls = 0; ls < S; ++ls) ma += affine_mu_part<S>(c, st, ls, at[ls], al[ls], aa);
         const double mua = group_sum(ma, c.gs) / m;
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
         const double smu = sg * mu;
         // ---- corrector
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) barrier_terms<S, true>(c, p, st, ls, smu);
+        for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, st, ls, at[ls], al[ls], smu);
         riccati_solve<S, false>(c, p, st, dx0, F_VN, M);
+        double dt[S][6], dl[S][6];
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, false, 0.0);
+        for (int ls = 0; ls < S; ++ls) corrector_dirs<S>(c, p, st, ls, at[ls], al[ls], smu, dt[ls], dl[ls], num, den);
         double alpha = p.frac * group_min(num / den, c.gs);
         alpha = fmin(alpha, 1.0);
         if (done) alpha = 0.0;
         rscale *= 1.0 - alpha;
-        // update (directions are recomputed from the same inputs before t, l change)
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
-            const double vu0 = st.f(F_VN, ls, 1), vu1 = st.f(F_VN, ls, 2);
-            directions<S, true>(c, p, st, ls, F_VN, smu, num, den, dummy, 0.0, true, alpha);
-            st.du(ls, 0) += alpha * (vu0 - st.du(ls, 0));
-            st.du(ls, 1) += alpha * (vu1 - st.du(ls, 1));
+            apply_step<S>(st, ls, dt[ls], dl[ls], alpha);
+            st.du(ls, 0) += alpha * (st.f(F_VN, ls, 1) - st.du(ls, 0));
+            st.du(ls, 1) += alpha * (st.f(F_VN, ls, 2) - st.du(ls, 1));
         }
     }
     return nit;
