@@ -340,7 +340,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
-    al(s->whist, 4 * 64 * 4);
+    al(s->whist, 4 * 1024 * 4);   // qsp_solver.hip PACK_KEYS_MAX
     al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);

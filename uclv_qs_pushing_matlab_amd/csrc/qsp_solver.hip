@@ -133,9 +133,18 @@ __device__ __forceinline__ int sidx(int i, int j) {
     return i == 0 ? j : (i == 1 ? 3 + j : (i == 2 ? 5 + j : 9));
 }
 
-// Wave-packing key of an instance from the IPM iteration count of its last QP: longest
-// first (LPT order), so a launch does not end on a tail of long waves.
-__device__ __forceinline__ int iters_key(int nit, int maxkey) { return maxkey - min(max(nit, 0), maxkey); }
+// Wave packing.  wnit holds an instance's last two IPM iteration counts (last | previous
+// << 8); the key orders by the last count, longest first (LPT, so a launch does not end on
+// a tail of long waves), ties by the one before.  The second level predicts the coming QP
+// better: over 50 SQP iterations of the bench workload (oracle counts, 3 instances per
+// wave) waves run 1.066x the mean iteration count instead of 1.095x with the last count
+// alone (1.239x unsorted).
+constexpr int PACK_KEYS_MAX = 1024;   // (qp_iters + 1)^2 keys; packing needs qp_iters <= 31
+__device__ __forceinline__ int pack_key(int packed, int maxkey) {
+    const int last = min(max(packed & 0xff, 0), maxkey), prev = min(max((packed >> 8) & 0xff, 0), maxkey);
+    return (maxkey - last) * (maxkey + 1) + (maxkey - prev);
+}
+__device__ __forceinline__ int pack_record(int old, int nit) { return ((old & 0xff) << 8) | (nit & 0xff); }
 
 // ------------------------------------------------------------- per-lane state
 // Registers hold what the horizon recursions read on every step (stage model,
@@ -856,6 +865,7 @@ __global__ void prologue_kernel(SolveArgs A) {
     double* U = A.wU + (size_t)i * N * 2;
     A.qp_iter[i] = 0;
     if (A.wdone) A.wdone[i] = 0;
+    if (A.wnit) A.wnit[i] = 0;
     if (!(A.flags & QSP_FLAG_CONTROLLER)) {
         for (int q = 0; q < (N + 1) * 4; ++q) X[q] = A.X_in[(size_t)i * (N + 1) * 4 + q];
         for (int q = 0; q < N * 2; ++q) U[q] = A.U_in[(size_t)i * N * 2 + q];
@@ -1148,11 +1158,13 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             A.sqp_iter[iv] = it;
         }
     }
-    if (A.whist && c.real && c.lig == 0) {
-        // wave-packing key of this instance for the next launch (sort_by_iters_kernel): the
-        // iteration count it records below (an instance that did not iterate keeps its old one)
-        const int rec = (MERIT || !(skip || failed)) ? nit : A.wnit[iv];
-        atomicAdd(&A.whist[(it & 1) * 64 + iters_key(rec, p.qp_iters)], 1);
+    if (A.wnit && c.real && c.lig == 0) {
+        // wave-packing record and key of this instance for the next launch
+        // (sort_by_iters_kernel); an instance that did not iterate keeps its record
+        const int old = A.wnit[iv];
+        const int rec = (MERIT || !(skip || failed)) ? pack_record(old, nit) : old;
+        A.wnit[iv] = rec;
+        if (A.whist) atomicAdd(&A.whist[(it & 1) * PACK_KEYS_MAX + pack_key(rec, p.qp_iters)], 1);
     }
     if constexpr (MERIT) {
         // QP solution (step, dynamics and bound multipliers) for the line-search kernel
@@ -1170,10 +1182,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 #pragma unroll
             for (int q = 0; q < 6; ++q) w[(Q_LAM + q) * tot] = c.lig < N ? st.lm(0, q) : 0.0;
         }
-        if (c.real && c.lig == 0) {
-            A.qp_iter[iv] += nit;
-            if (A.wnit) A.wnit[iv] = nit;
-        }
+        if (c.real && c.lig == 0) A.qp_iter[iv] += nit;
         return;
     }
     const bool last = it + 1 >= p.sqp_iters;
@@ -1208,44 +1217,68 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             U[2 * k] += st.du(ls, 0);
             U[2 * k + 1] += st.du(ls, 1);
         }
-        if (k == 0) {
-            A.qp_iter[iv] += nit;
-            if (A.wnit) A.wnit[iv] = nit;
-        }
+        if (k == 0) A.qp_iter[iv] += nit;
     }
 }
 
-// Counting sort of the instances by the IPM iteration count of their last QP (keys
-// 0..qp_iters), in one pass over the instances: the histogram of the keys was accumulated
-// by the QP launch itself (whist, parity q), each block places its instances at the key's
-// prefix plus a block offset taken from the running counters, then clears the other
-// parity's histogram and counters for the next launch.  The order inside a key is
-// arbitrary and does not affect any result (instances are independent).
+// Counting sort of the instances by their packing key (pack_key) in one pass over the
+// instances: the histogram of the keys was accumulated by the QP launch itself (whist,
+// parity q); every block forms the exclusive prefix of the histogram (a block-wide scan),
+// places its instances at the key's prefix plus a block offset taken from the running
+// counters, and block 0 clears the other parity's histogram and counters for the next
+// launch.  The order inside a key is arbitrary and does not affect any result (instances
+// are independent).
 __global__ void __launch_bounds__(256) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm,
                                                             int32_t* whist, int q) {
-    __shared__ int pre[64], lcount[64], lbase[64];
+    constexpr int KPT = PACK_KEYS_MAX / 256;   // keys per thread in the prefix scan
+    __shared__ int pre[PACK_KEYS_MAX], lcount[PACK_KEYS_MAX], part[256];
     const int tid = threadIdx.x;
-    int32_t* hist = whist + q * 64;
-    int32_t* run = whist + 128 + q * 64;
-    if (tid < 64) lcount[tid] = 0;
-    if (tid == 0) {
-        int acc = 0;
-        for (int k = 0; k <= maxkey; ++k) { pre[k] = acc; acc += hist[k]; }
+    const int nkeys = (maxkey + 1) * (maxkey + 1);
+    const int32_t* hist = whist + q * PACK_KEYS_MAX;
+    int32_t* run = whist + (2 + q) * PACK_KEYS_MAX;
+    int h[KPT], sum = 0;
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+        const int k = tid * KPT + r;
+        h[r] = k < nkeys ? hist[k] : 0;
+        sum += h[r];
+        lcount[k] = 0;
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {   // inclusive scan of the per-thread sums
+        const int v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int acc = part[tid] - sum;
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+        pre[tid * KPT + r] = acc;
+        acc += h[r];
     }
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + tid;
     int key = 0, pos = 0;
     if (i < B) {
-        key = iters_key(nit[i], maxkey);
+        key = pack_key(nit[i], maxkey);
         pos = atomicAdd(&lcount[key], 1);
     }
     __syncthreads();
-    if (tid <= maxkey && lcount[tid] > 0) lbase[tid] = pre[tid] + atomicAdd(&run[tid], lcount[tid]);
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+        const int k = tid * KPT + r;
+        if (lcount[k] > 0) pre[k] += atomicAdd(&run[k], lcount[k]);
+    }
     __syncthreads();
-    if (i < B) perm[lbase[key] + pos] = i;
-    if (blockIdx.x == 0 && tid < 64) {
-        whist[(1 - q) * 64 + tid] = 0;
-        whist[128 + (1 - q) * 64 + tid] = 0;
+    if (i < B) perm[pre[key] + pos] = i;
+    if (blockIdx.x == 0) {
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            whist[(1 - q) * PACK_KEYS_MAX + tid * KPT + r] = 0;
+            whist[(3 - q) * PACK_KEYS_MAX + tid * KPT + r] = 0;
+        }
     }
 }
 
@@ -1654,13 +1687,13 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
-    const bool sorted = a.wperm && a.wnit && a.whist && a.p.qp_iters < 64;
+    const bool sorted = a.wperm && a.wnit && a.whist && (a.p.qp_iters + 1) * (a.p.qp_iters + 1) <= PACK_KEYS_MAX;
     SolveArgs as = a;
     if (!sorted) as.whist = nullptr;
     if (e == hipSuccess && sorted) {
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemsetAsync(a.whist, 0, 4 * 64 * sizeof(int32_t), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(a.whist, 0, 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
     for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
