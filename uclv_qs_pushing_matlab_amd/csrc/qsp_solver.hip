@@ -150,7 +150,7 @@ __device__ __forceinline__ int pack_record(int old, int nit) { return ((old & 0x
 // Registers hold what the horizon recursions read on every step (stage model,
 // gradient, Riccati factors); LDS holds what only the stage-parallel phases touch
 // (iterate, slacks/multipliers, barrier terms, QP solution pieces).
-constexpr int BLOCK = 256;                 // threads per workgroup (4 waves)
+constexpr int BLOCK = 64;                  // threads per workgroup: one wave (see launch_qp_step)
 enum LdsField : int {
     F_T = 0,      // 6  slacks        s_lo s_hi un_lo un_hi ut_lo ut_hi
     F_LM = 6,     // 6  multipliers
