@@ -1292,7 +1292,7 @@ __global__ void iota_kernel(int B, int32_t* perm) {
 // its directional derivative; alpha <- ls_alpha_red * alpha until
 // phi(alpha) <= phi(0) + ls_eps alpha dphi or alpha would drop below ls_alpha_min (then
 // the last alpha tried is taken); X, U, PI, LAM updated with that alpha.
-__global__ void __launch_bounds__(256) merit_ls_kernel(SolveArgs A) {
+__global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     const SolveParams& p = A.p;
     Ctx c;
     c.lane = threadIdx.x & 63;
@@ -1675,7 +1675,7 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(merit_ls_kernel, dim3((waves * 64 + 255) / 256), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(merit_ls_kernel, dim3(waves), dim3(64), 0, stream, a);   // one wave per workgroup
     return hipGetLastError();
 }
 
