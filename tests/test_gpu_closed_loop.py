@@ -103,3 +103,18 @@ def test_closed_loop_main_m_sqp():
         np.testing.assert_allclose(r["U"][lane], g["U"], rtol=0, atol=1e-7)
         np.testing.assert_allclose(r["X"][lane], g["X"], rtol=0, atol=1e-7)
         assert np.mean(r["status"][lane] == g["status"]) > 0.95
+
+
+def test_c_host_closed_loop(tmp_path):
+    """The same configs[0] closed loop from a plain-C host (integration/c/qsp_demo.c, built by
+    __graft_entry__.build()) through the C ABI alone, against the committed golden trace."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "integration", "c", "qsp_demo")
+    ply = os.path.join(root, "uclv_qs_pushing_matlab_amd", "data", "planar_surface_santal_36_uniformed.ply")
+    out = tmp_path / "u.txt"
+    assert os.path.exists(exe), "integration/c/qsp_demo not built (run __graft_entry__.build())"
+    r = subprocess.run([exe, ply, str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    g = np.load(os.path.join(GOLDEN, "config1_rti_full.npz"))
+    np.testing.assert_allclose(np.loadtxt(out), g["U"], rtol=0, atol=1e-8)
