@@ -104,11 +104,12 @@ static void fill_params(qsp_solver* s) {
 }
 
 static int auto_S(int N) {
-    // One stage per lane keeps the QP kernel at 2 waves/SIMD with its closed-loop walks;
-    // two stages per lane spill into AGPRs at 1 wave/SIMD and lose at every measured
-    // horizon (scripts/layout_sweep.sh, round 1: N = 10 1.21M vs 1.02M, N = 20 428k vs 325k,
-    // N = 50 (B = 16 384) 55.1k vs 54.2k solves/s).  S = 2 remains for N + 1 > 64.
-    return N + 1 <= 64 ? 1 : 2;
+    // One stage per lane keeps the QP kernel at 2 waves/SIMD with its closed-loop walks and
+    // wins while a wavefront still holds two or more instances; once one stage per lane leaves
+    // a single instance per wave (N + 1 > 32), two stages per lane (1 wave/SIMD, 2-3 instances
+    // per wave) win.  scripts/layout_sweep.sh, round 1 (one-wave workgroups): N = 10 1.32M vs
+    // 1.17M, N = 20 493k vs 422k, N = 50 (B = 16 384) 62.6k vs 70.0k solves/s for S = 1 vs 2.
+    return N + 1 <= 32 ? 1 : 2;
 }
 
 // Binary little-endian PLY with float32 vertex properties (the reference's cad_models/*.ply).
