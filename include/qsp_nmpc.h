@@ -172,6 +172,13 @@ int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int3
 /* ------------------------------------------------ device-resident fast path */
 int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* hip_stream);
 int qsp_synchronize(qsp_solver* s);
+/* The SQP loop of a solve can run in two parts, each half of the lanes iterating on its own
+ * HIP stream (forked from and joined back into the solve's stream), so that the tail of one
+ * half's QP launch overlaps the other half's work.  Results are bit-identical either way.
+ * parts: 0 = auto (two once each half fills the GPU several times over), 1, or 2.  No acados
+ * counterpart (an execution choice of the batched engine).  get: the count the next solve uses. */
+int qsp_set_stream_parts(qsp_solver* s, int32_t parts);
+int qsp_get_stream_parts(qsp_solver* s, int32_t* parts);
 /* Per-kernel timing (acados' time_lin / time_qp split).  qsp_set_kernel_timing(s, n) pre-creates
  * HIP events for the next n solves (0 disables): every kernel boundary of each solve is then
  * recorded on the solve's stream.  qsp_get_kernel_times synchronises the recorded events and

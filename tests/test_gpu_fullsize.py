@@ -52,6 +52,33 @@ def test_config3_shuffle_invariance_and_bounds():
     assert np.mean(viol > 1e-9) < 2e-4, (np.sum(viol > 1e-9), np.sort(viol)[-5:])
 
 
+@pytest.mark.parametrize("nlp_mode,B,K", [(0, 65536, 50), (1, 8192, 30)])
+def test_two_stream_parts_bit_identical(nlp_mode, B, K):
+    """The SQP loop split over two HIP streams (qsp_set_stream_parts) gives every lane the
+    same bits as the single-stream loop: u0, iterate, multipliers, status, iteration counts."""
+    from bench import make_inputs
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N = 20
+    x0, yref, yref_e, sid, traj = make_inputs(B, N, 20250303 + 3)
+    s = OcpSolver(N=N, batch=B, sqp_iters=K, nlp_solver_type="SQP" if nlp_mode else "SQP_RTI")
+    s.set_shapes([make_shape(n) for n in NAMES])
+    s.set_reference_trajectory(traj)
+    s.set_shape_ids(sid)
+    if nlp_mode == 0:
+        assert s.stream_parts() == 2          # auto: the bench batch runs in two parts
+    out = {}
+    for parts in (1, 2):
+        s.set_stream_parts(parts)
+        assert s.stream_parts() == parts
+        s.controller_reset()
+        u = s.controller_solve(x0, 1)
+        out[parts] = [u] + [s.get(f) for f in ("x", "u", "pi", "status", "sqp_iter", "qp_iter")]
+    s.close()
+    for a, b in zip(out[1], out[2]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_config4_batch_one_device():
     from bench import make_inputs
     B, N = 262144, 20

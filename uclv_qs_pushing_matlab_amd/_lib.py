@@ -87,6 +87,8 @@ _SIGS = {
     "qsp_closed_loop": [_P, _P, _P, _I, _P, _P, _P, _P],
     "qsp_solve_device": [_P, C.POINTER(DeviceIO), _P],
     "qsp_synchronize": [_P],
+    "qsp_set_stream_parts": [_P, _I],
+    "qsp_get_stream_parts": [_P, C.POINTER(_I)],
     "qsp_set_kernel_timing": [_P, _I],
     "qsp_get_kernel_times": [_P, C.POINTER(_D), C.POINTER(_I)],
     "qsp_eval_spline": [_P, _I, _P, _P, _P, _P, _P, _P],

@@ -67,14 +67,24 @@ struct qsp_solver {
     std::vector<hipEvent_t> kev;   // kernel-timing pool (qsp_set_kernel_timing)
     int kev_used = 0;
     std::vector<int> kev_solves;   // event offset of each timed solve
+    std::vector<int> kev_split;    // ... and whether its SQP loop ran in two parts
+    // two-stream SQP loop (launch_sqp): second stream, fork/join events, requested parts (0 = auto)
+    SqpStreams split;
+    int parts_req = 0;
 };
 
 // --------------------------------------------------------------- helpers
+static const SqpStreams* sqp_split(qsp_solver* s) {
+    s->split.parts = s->parts_req > 0 ? s->parts_req : sqp_parts_auto(s->o.batch, s->o.N, s->S);
+    return &s->split;
+}
+
 // events for one timed solve (nullptr when timing is off or the pool is used up)
 static hipEvent_t* take_kernel_events(qsp_solver* s) {
     const int per = 2 * s->o.sqp_iters + 3;
     if (s->kev.empty() || s->kev_used + per > (int)s->kev.size()) return nullptr;
     s->kev_solves.push_back(s->kev_used);
+    s->kev_split.push_back(sqp_split(s)->parts == 2 ? 1 : 0);
     hipEvent_t* e = s->kev.data() + s->kev_used;
     s->kev_used += per;
     return e;
@@ -189,7 +199,7 @@ static SolveArgs make_args(qsp_solver* s) {
 
 static int run_timed(qsp_solver* s, const SolveArgs& a) {
     HIPCHK(hipEventRecord(s->ev0, s->stream));
-    HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s)));
+    HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s), sqp_split(s)));
     HIPCHK(hipEventRecord(s->ev1, s->stream));
     HIPCHK(hipEventSynchronize(s->ev1));
     HIPCHK(hipEventElapsedTime(&s->last_ms, s->ev0, s->ev1));
@@ -317,6 +327,9 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&s->ev0);
     if (e == hipSuccess) e = hipEventCreate(&s->ev1);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->split.aux, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->split.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->split.join, hipEventDisableTiming);
     const size_t B = o->batch, N = o->N;
     auto al = [&](DevBuf& b, size_t bytes) { if (e == hipSuccess) e = b.ensure(bytes); };
     al(s->shape_id, B * 4);
@@ -341,7 +354,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
-    al(s->whist, 4 * 1024 * 4);   // qsp_solver.hip PACK_KEYS_MAX
+    al(s->whist, 2 * 4 * 1024 * 4);   // per part of the SQP loop; qsp_solver.hip PACK_KEYS_MAX
     al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);
@@ -388,6 +401,9 @@ int qsp_destroy(qsp_solver* s) {
     for (hipEvent_t e : s->kev) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->split.fork) (void)hipEventDestroy(s->split.fork);
+    if (s->split.join) (void)hipEventDestroy(s->split.join);
+    if (s->split.aux) (void)hipStreamDestroy(s->split.aux);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return QSP_OK;
@@ -703,7 +719,7 @@ int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int3
     const SolveArgs a = controller_args(s);
     for (int32_t t = 0; t < n_steps; ++t) {
         HIPCHK(launch_controller_step(s, t));                                  // y_ref for index0 + t
-        HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s)));      // NMPC_controller.solve
+        HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s), sqp_split(s)));   // NMPC_controller.solve
         HIPCHK(launch_plant(s->shapes.as<ShapeDev>(), s->shape_id.as<int32_t>(), (int)B, s->o.Ts, s->x0.as<double>(),
                             s->u0.as<double>(), s->status.as<int32_t>(), t, n_steps,
                             (nz && t + 1 < n_steps) ? nz + (size_t)(t + 1) * B * 4 : nullptr, dX.as<double>(),
@@ -745,7 +761,19 @@ int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
         a.warm_valid = io->warm_valid;
     }
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    HIPCHK(launch_sqp(a, s->S, st, take_kernel_events(s)));
+    HIPCHK(launch_sqp(a, s->S, st, take_kernel_events(s), sqp_split(s)));
+    return QSP_OK;
+}
+
+int qsp_set_stream_parts(qsp_solver* s, int32_t parts) {
+    if (!s || parts < 0 || parts > 2) return fail(QSP_ERR_ARG, "qsp_set_stream_parts: parts must be 0 (auto), 1 or 2");
+    s->parts_req = parts;
+    return QSP_OK;
+}
+
+int qsp_get_stream_parts(qsp_solver* s, int32_t* parts) {
+    if (!s || !parts) return fail(QSP_ERR_ARG, "qsp_get_stream_parts: null argument");
+    *parts = sqp_split(s)->parts;
     return QSP_OK;
 }
 
@@ -755,6 +783,7 @@ int qsp_set_kernel_timing(qsp_solver* s, int32_t max_solves) {
     for (hipEvent_t e : s->kev) HIPCHK(hipEventDestroy(e));
     s->kev.clear();
     s->kev_solves.clear();
+    s->kev_split.clear();
     s->kev_used = 0;
     const size_t n = (size_t)max_solves * (2 * s->o.sqp_iters + 3);
     for (size_t i = 0; i < n; ++i) {
@@ -770,11 +799,15 @@ int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
     HIPCHK(hipSetDevice(s->o.device));
     for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; }
     const int K = s->o.sqp_iters;
-    for (int off : s->kev_solves) {
-        hipEvent_t* e = s->kev.data() + off;
+    for (size_t j = 0; j < s->kev_solves.size(); ++j) {
+        hipEvent_t* e = s->kev.data() + s->kev_solves[j];
         HIPCHK(hipEventSynchronize(e[2 * K + 2]));
         float t;
         HIPCHK(hipEventElapsedTime(&t, e[0], e[1])); ms[0] += t; launches[0] += 1;
+        if (s->kev_split[j]) {
+            // two-stream loop: timed as a whole, one "launch" per SQP iteration (sorts included)
+            HIPCHK(hipEventElapsedTime(&t, e[1], e[2 * K + 1])); ms[2] += t; launches[2] += K;
+        } else
         for (int it = 0; it < K; ++it) {
             HIPCHK(hipEventElapsedTime(&t, e[1 + 2 * it], e[2 + 2 * it])); ms[1] += t; launches[1] += 1;
             HIPCHK(hipEventElapsedTime(&t, e[2 + 2 * it], e[3 + 2 * it])); ms[2] += t; launches[2] += 1;
@@ -782,6 +815,7 @@ int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
         HIPCHK(hipEventElapsedTime(&t, e[2 * K + 1], e[2 * K + 2])); ms[3] += t; launches[3] += 1;
     }
     s->kev_solves.clear();
+    s->kev_split.clear();
     s->kev_used = 0;
     return QSP_OK;
 }

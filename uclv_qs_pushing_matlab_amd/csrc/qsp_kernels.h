@@ -14,6 +14,10 @@ namespace qsp {
 struct SolveArgs {
     SolveParams p;
     int32_t B;
+    // instance range [i0, i0 + nI) of one QP / line-search launch: launch_sqp may split the
+    // batch into parts iterated on their own HIP streams (whist then points at the part's own
+    // histogram); strides of the SoA workspace stay B(N+1)
+    int32_t i0, nI;
     uint32_t flags;
     const ShapeDev* shapes;
     int32_t n_shapes;
@@ -54,9 +58,22 @@ struct SolveArgs {
 
 
 int lanes_per_instance(int N, int S);
+// Two-stream split of the SQP loop (SqpStreams::parts == 2): the instances are halved and
+// each half runs its own (sort, qp_step) sequence on its own stream, so the launch tail of
+// one half's QP overlaps the other half's work.  Results are bit-identical to the
+// single-stream loop (instances are independent).  Streams and events owned by the handle.
+struct SqpStreams {
+    hipStream_t aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    int parts = 1;   // 1 or 2
+};
 // ev (optional): 2*sqp_iters + 3 events recorded on `stream` at every kernel boundary
-// (prologue | linearize, qp_step x sqp_iters | epilogue), for per-kernel timing.
-hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr);
+// (prologue | sort, qp_step x sqp_iters | epilogue), for per-kernel timing.  With two parts
+// only ev[0], ev[1] (fork), ev[2K+1] (join) and ev[2K+2] are recorded: the SQP loop is timed
+// as a whole (qsp_get_kernel_times then reports K qp_step "launches" = SQP iterations).
+hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr,
+                      const SqpStreams* split = nullptr);
+int sqp_parts_auto(int B, int N, int S);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
 hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
                                    hipStream_t stream);

@@ -1043,10 +1043,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     c.gs.init(c.base, c.L);
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
-    c.real = (c.grp < G) && (c.inst < A.B);
+    c.real = (c.grp < G) && (c.inst < A.nI);
     // instances are packed into waves in the order of their previous IPM iteration count
     // (sort_by_iters_kernel), so the instances sharing a wave finish together
-    const int slot = c.real ? c.inst : A.B - 1;
+    const int slot = A.i0 + (c.real ? c.inst : A.nI - 1);
     const int iv = A.wperm ? A.wperm[slot] : slot;
     const int N = p.N;
     const size_t tot = (size_t)A.B * (N + 1);
@@ -1227,9 +1227,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 // places its instances at the key's prefix plus a block offset taken from the running
 // counters, and block 0 clears the other parity's histogram and counters for the next
 // launch.  The order inside a key is arbitrary and does not affect any result (instances
-// are independent).
-__global__ void __launch_bounds__(256) sort_by_iters_kernel(int B, int maxkey, const int32_t* nit, int32_t* perm,
-                                                            int32_t* whist, int q) {
+// are independent).  Sorts the instance range [i0, i0 + B) into perm[i0 ...] (one part of a
+// split SQP loop, with the part's own whist).
+__global__ void __launch_bounds__(256) sort_by_iters_kernel(int i0, int B, int maxkey, const int32_t* nit,
+                                                            int32_t* perm, int32_t* whist, int q) {
     constexpr int KPT = PACK_KEYS_MAX / 256;   // keys per thread in the prefix scan
     __shared__ int pre[PACK_KEYS_MAX], lcount[PACK_KEYS_MAX], part[256];
     const int tid = threadIdx.x;
@@ -1262,7 +1263,7 @@ __global__ void __launch_bounds__(256) sort_by_iters_kernel(int B, int maxkey, c
     const int i = blockIdx.x * blockDim.x + tid;
     int key = 0, pos = 0;
     if (i < B) {
-        key = pack_key(nit[i], maxkey);
+        key = pack_key(nit[i0 + i], maxkey);
         pos = atomicAdd(&lcount[key], 1);
     }
     __syncthreads();
@@ -1272,7 +1273,7 @@ __global__ void __launch_bounds__(256) sort_by_iters_kernel(int B, int maxkey, c
         if (lcount[k] > 0) pre[k] += atomicAdd(&run[k], lcount[k]);
     }
     __syncthreads();
-    if (i < B) perm[pre[key] + pos] = i;
+    if (i < B) perm[i0 + pre[key] + pos] = i0 + i;
     if (blockIdx.x == 0) {
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
@@ -1305,8 +1306,8 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     c.gs.init(c.base, c.L);
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
-    c.real = (c.grp < G) && (c.inst < A.B);
-    const int iv = c.real ? c.inst : A.B - 1;
+    c.real = (c.grp < G) && (c.inst < A.nI);
+    const int iv = A.i0 + (c.real ? c.inst : A.nI - 1);
     const int N = p.N;
     const int k = c.lig <= N ? c.lig : N;
     const bool stg = k < N;
@@ -1645,7 +1646,7 @@ template <int S, bool LIN>
 static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
-    const int waves = (a.B + G - 1) / G;
+    const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
     const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN>, lds_bytes<S>(), attr);
@@ -1667,10 +1668,10 @@ int lanes_per_instance(int N, int S) { return (N + S) / S; }
 static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = a.p.N + 1;
     const int G = 64 / L;
-    const int waves = (a.B + G - 1) / G;
+    const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
-    const hipError_t ea = lds_attr_once((const void*)qp_step_kernel<1, true, true>, lds_bytes<1>(), attr);
+    const hipError_t ea =lds_attr_once((const void*)qp_step_kernel<1, true, true>, lds_bytes<1>(), attr);
     if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
     hipError_t e = hipGetLastError();
@@ -1679,9 +1680,42 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     return hipGetLastError();
 }
 
-hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev) {
+// Two parts once each half still fills the 2 048 wave slots of the chip (2 waves/SIMD) about
+// four times over; below that a launch is mostly its own tail and the halves gain nothing.
+// Measured at the bench workload (B = 65 536, N = 20, 21 846 waves; scripts/two_streams.py
+// with one handle per part): 493k solves/s in one part, 513k in two, 514k in four.
+int sqp_parts_auto(int B, int N, int S) {
+    const int G = 64 / lanes_per_instance(N, S);
+    const long waves = ((long)B + G - 1) / G;
+    return waves >= 8 * 2048 ? 2 : 1;
+}
+
+// One part's SQP loop on `stream`: (packing sort, QP [+ line search]) x sqp_iters over the
+// instance range of `as`.  mark(): kernel-boundary events (single-part loop only).
+template <class Mark>
+static hipError_t sqp_iteration(const SolveArgs& as, int S, bool sorted, int it, hipStream_t stream, Mark&& mark) {
+    hipError_t e = hipSuccess;
+    if (sorted && it > 0) {
+        hipLaunchKernelGGL(sort_by_iters_kernel, dim3((as.nI + 255) / 256), dim3(256), 0, stream, as.i0, as.nI,
+                           as.p.qp_iters, as.wnit, as.wperm, as.whist, (it - 1) & 1);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = mark();
+    if (e == hipSuccess)
+        e = as.p.nlp_mode == 1 ? launch_sqp_merit(as, it, stream) : launch_qp_any(as, S, it, stream, true);
+    if (e == hipSuccess) e = mark();
+    return e;
+}
+
+hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev, const SqpStreams* split) {
+    const int G = 64 / lanes_per_instance(a.p.N, S);
+    // part boundary on a whole wave of the first part
+    const int h = (a.B / 2 / G) * G;
+    const bool two = split && split->aux && split->fork && split->join && split->parts == 2 && h > 0;
+    const int K = a.p.sqp_iters;
     int ne = 0;
     auto mark = [&]() { return ev ? hipEventRecord(ev[ne++], stream) : hipSuccess; };
+    auto nomark = []() { return hipSuccess; };
     const unsigned gb = (unsigned)((a.B + 127) / 128);
     hipError_t e = mark();
     if (e != hipSuccess) return e;
@@ -1689,23 +1723,34 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     e = hipGetLastError();
     const bool sorted = a.wperm && a.wnit && a.whist && (a.p.qp_iters + 1) * (a.p.qp_iters + 1) <= PACK_KEYS_MAX;
     SolveArgs as = a;
+    as.i0 = 0;
+    as.nI = a.B;
     if (!sorted) as.whist = nullptr;
     if (e == hipSuccess && sorted) {
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemsetAsync(a.whist, 0, 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(a.whist, 0, (two ? 2 : 1) * 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
-    for (int it = 0; it < a.p.sqp_iters && e == hipSuccess; ++it) {
-        if (sorted && it > 0) {
-            hipLaunchKernelGGL(sort_by_iters_kernel, dim3((a.B + 255) / 256), dim3(256), 0, stream, a.B, a.p.qp_iters,
-                               a.wnit, a.wperm, a.whist, (it - 1) & 1);
-            e = hipGetLastError();
-            if (e != hipSuccess) break;
+    if (!two) {
+        for (int it = 0; it < K && e == hipSuccess; ++it) e = sqp_iteration(as, S, sorted, it, stream, mark);
+    } else {
+        // fork: the second half waits for the prologue, then both halves iterate independently
+        SolveArgs a0 = as, a1 = as;
+        a0.nI = h;
+        a1.i0 = h;
+        a1.nI = a.B - h;
+        if (sorted) a1.whist = a.whist + 4 * PACK_KEYS_MAX;
+        if (e == hipSuccess) e = hipEventRecord(split->fork, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(split->aux, split->fork, 0);
+        for (int it = 0; it < K && e == hipSuccess; ++it) {
+            e = sqp_iteration(a0, S, sorted, it, stream, nomark);
+            if (e == hipSuccess) e = sqp_iteration(a1, S, sorted, it, split->aux, nomark);
         }
-        const bool merit = a.p.nlp_mode == 1;
-        if (e == hipSuccess) e = mark();
-        if (e == hipSuccess) e = merit ? launch_sqp_merit(as, it, stream) : launch_qp_any(as, S, it, stream, true);
+        if (e == hipSuccess) e = hipEventRecord(split->join, split->aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, split->join, 0);
+        ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
     }
     if (e != hipSuccess) return e;
@@ -1717,7 +1762,10 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
 
 // One QP (qsp_qp_solve): the workspace already holds the stage data.
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream) {
-    return launch_qp_any(a, S, a.p.sqp_iters - 1, stream, false);
+    SolveArgs as = a;
+    as.i0 = 0;
+    as.nI = a.B;
+    return launch_qp_any(as, S, a.p.sqp_iters - 1, stream, false);
 }
 
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,

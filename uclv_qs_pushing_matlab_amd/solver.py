@@ -282,6 +282,15 @@ class OcpSolver:
     def synchronize(self):
         check(self._L.qsp_synchronize(self._h), "qsp_synchronize")
 
+    def set_stream_parts(self, parts):
+        """SQP loop in 1 or 2 parts on their own HIP streams (0 = auto); results are identical."""
+        check(self._L.qsp_set_stream_parts(self._h, int(parts)), "qsp_set_stream_parts")
+
+    def stream_parts(self):
+        p = C.c_int32()
+        check(self._L.qsp_get_stream_parts(self._h, C.byref(p)), "qsp_get_stream_parts")
+        return p.value
+
     def set_kernel_timing(self, max_solves):
         """Record HIP events at every kernel boundary of the next `max_solves` solves."""
         check(self._L.qsp_set_kernel_timing(self._h, int(max_solves)), "qsp_set_kernel_timing")
