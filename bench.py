@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--sqp-iters", type=int, default=50)
     ap.add_argument("--qp-iters", type=int, default=20)
     ap.add_argument("--stages-per-lane", type=int, default=0)
+    ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
+                    help="SQP loop in 1 or 2 lane halves on their own HIP streams (0 = the library's auto choice)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
@@ -145,6 +147,8 @@ def main():
                        device=gpu, nlp_solver_type=args.nlp)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
+    solver.set_stream_parts(args.stream_parts)
+    parts = solver.stream_parts()
 
     t = lambda a, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
     d_x0, d_yref, d_yref_e = t(x0), t(yref), t(yref_e)
@@ -199,7 +203,12 @@ def main():
     status = d_st.cpu().numpy()
     u0 = d_u0.cpu().numpy()
     flops_solve = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())   # all lanes, one solve
-    # dominant kernel: qp_step (one launch = one SQP iteration's QP for every lane of the shard)
+    # dominant kernel: qp_step (one launch = one SQP iteration's QP for every lane of the shard).
+    # With two stream parts the two half launches of an SQP iteration overlap each other and
+    # the next iteration's, so the library times the whole loop (fork -> join on the launch
+    # stream, packing sorts included) and reports K "launches": launch_ms_avg is then the loop
+    # time per SQP iteration over the whole shard (rocprof: union of the qp_step intervals / K,
+    # scripts/ktrace_union.py)
     qp_ms, qp_n = ktimes["qp_step"]
     qp_avg_s = qp_ms / max(qp_n, 1) * 1e-3
     qp_flops_launch = float(qp_iter.astype(np.float64).sum()) * N * FLOP_IPM_STAGE / K
@@ -227,7 +236,8 @@ def main():
                                + ", cold-start NMPC_controller.solve per lane",
                    "global_batch": B * world, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
                    "nlp_solver_type": args.nlp,
-                   "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout},
+                   "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
+                              "stream_parts": parts},
                    "parallelism": f"dp{world} (independent lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
@@ -238,6 +248,8 @@ def main():
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                      "flops_per_launch": qp_flops_launch, "launch_ms_avg": qp_avg_s * 1e3,
+                     "launch": ("one SQP iteration over the shard: two concurrent half launches on two streams, "
+                                "timed fork -> join" if parts == 2 else "one qp_step launch over the shard"),
                      "whole_solve_tflops": flops_solve / avg_kern_s / 1e12},
     }
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

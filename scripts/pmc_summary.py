@@ -19,6 +19,7 @@ ap.add_argument("--kernel", default="qp_step_kernel")
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--N", type=int, default=20)
 ap.add_argument("--sqp-iters", type=int, default=50)
+ap.add_argument("--parts", type=int, default=2, help="stream parts of the profiled solves (bench.py layout)")
 args = ap.parse_args()
 
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -39,10 +40,13 @@ for k, d in tot.items():
 if args.json:
     ks = [k for k in tot if args.kernel in k]
     assert ks, f"no {args.kernel} dispatches"
-    fetch = sum(tot[k]["FETCH_SIZE"] for k in ks) / sum(len(ndisp[k]["FETCH_SIZE"]) for k in ks)
-    write = sum(tot[k]["WRITE_SIZE"] for k in ks) / sum(len(ndisp[k]["WRITE_SIZE"]) for k in ks)
+    # per SQP iteration over the whole batch: with --parts 2 every iteration is two half
+    # launches (one per stream), so the per-dispatch counters are summed over `parts` dispatches
+    fetch = sum(tot[k]["FETCH_SIZE"] for k in ks) / (sum(len(ndisp[k]["FETCH_SIZE"]) for k in ks) / args.parts)
+    write = sum(tot[k]["WRITE_SIZE"] for k in ks) / (sum(len(ndisp[k]["WRITE_SIZE"]) for k in ks) / args.parts)
     rd, wr = fetch * 1024 * 2, write * 1024
     out = {"kernel": args.kernel, "batch": args.batch, "N": args.N, "sqp_iters": args.sqp_iters,
+           "stream_parts": args.parts, "per": "SQP iteration over the whole batch (= bench roofline launch)",
            "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
            "raw_FETCH_SIZE_KiB": fetch, "raw_WRITE_SIZE_KiB": write,
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024"}

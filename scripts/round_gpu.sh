@@ -15,6 +15,8 @@ tail -2 $R/tests.log
 if [ -z "$SKIP_PROF" ]; then
   echo "kernel trace"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/kt -o kt -- python3 bench.py --no-cpu --steps 3 --warmup 1 > $R/kt_bench.json 2> $R/kt_bench.err || exit $?
+  python scripts/ktrace_union.py $R/kt --parts 2 > $R/kt_union.txt || exit $?
+  cat $R/kt_union.txt
   echo "pmc"
   OUT=$R/pmc bash scripts/prof_pmc.sh || exit $?
   cp $R/pmc/pmc_traffic.json profiles/pmc_traffic.json
