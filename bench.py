@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--qp-iters", type=int, default=20)
     ap.add_argument("--stages-per-lane", type=int, default=0)
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
-                    help="SQP loop in 1 or 2 lane halves on their own HIP streams (0 = the library's auto choice)")
+                    help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
@@ -248,8 +248,8 @@ def main():
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                      "flops_per_launch": qp_flops_launch, "launch_ms_avg": qp_avg_s * 1e3,
-                     "launch": ("one SQP iteration over the shard: two concurrent half launches on two streams, "
-                                "timed fork -> join" if parts == 2 else "one qp_step launch over the shard"),
+                     "launch": (f"one SQP iteration over the shard: {parts} concurrent part launches on {parts} streams, "
+                                "timed fork -> join" if parts > 1 else "one qp_step launch over the shard"),
                      "whole_solve_tflops": flops_solve / avg_kern_s / 1e12},
     }
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -175,7 +175,7 @@ int qsp_synchronize(qsp_solver* s);
 /* The SQP loop of a solve can run in two parts, each half of the lanes iterating on its own
  * HIP stream (forked from and joined back into the solve's stream), so that the tail of one
  * half's QP launch overlaps the other half's work.  Results are bit-identical either way.
- * parts: 0 = auto (two once each half fills the GPU several times over), 1, or 2.  No acados
+ * parts: 0 = auto (two once the batch fills the GPU's wave slots), 1, or 2.  No acados
  * counterpart (an execution choice of the batched engine).  get: the count the next solve uses. */
 int qsp_set_stream_parts(qsp_solver* s, int32_t parts);
 int qsp_get_stream_parts(qsp_solver* s, int32_t* parts);

@@ -84,7 +84,7 @@ static hipEvent_t* take_kernel_events(qsp_solver* s) {
     const int per = 2 * s->o.sqp_iters + 3;
     if (s->kev.empty() || s->kev_used + per > (int)s->kev.size()) return nullptr;
     s->kev_solves.push_back(s->kev_used);
-    s->kev_split.push_back(sqp_split(s)->parts == 2 ? 1 : 0);
+    s->kev_split.push_back(sqp_split(s)->parts > 1 ? 1 : 0);
     hipEvent_t* e = s->kev.data() + s->kev_used;
     s->kev_used += per;
     return e;
@@ -327,9 +327,11 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&s->ev0);
     if (e == hipSuccess) e = hipEventCreate(&s->ev1);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->split.aux, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->split.fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->split.join, hipEventDisableTiming);
+    for (int q = 0; q < SQP_MAX_PARTS - 1; ++q) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->split.aux[q], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->split.join[q], hipEventDisableTiming);
+    }
     const size_t B = o->batch, N = o->N;
     auto al = [&](DevBuf& b, size_t bytes) { if (e == hipSuccess) e = b.ensure(bytes); };
     al(s->shape_id, B * 4);
@@ -354,7 +356,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
-    al(s->whist, 2 * 4 * 1024 * 4);   // per part of the SQP loop; qsp_solver.hip PACK_KEYS_MAX
+    al(s->whist, SQP_MAX_PARTS * 4 * 1024 * 4);   // per part of the SQP loop; qsp_solver.hip PACK_KEYS_MAX
     al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
         al(s->wnlp, B * (N + 1) * 20 * 8);
@@ -402,8 +404,10 @@ int qsp_destroy(qsp_solver* s) {
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->split.fork) (void)hipEventDestroy(s->split.fork);
-    if (s->split.join) (void)hipEventDestroy(s->split.join);
-    if (s->split.aux) (void)hipStreamDestroy(s->split.aux);
+    for (int q = 0; q < SQP_MAX_PARTS - 1; ++q) {
+        if (s->split.join[q]) (void)hipEventDestroy(s->split.join[q]);
+        if (s->split.aux[q]) (void)hipStreamDestroy(s->split.aux[q]);
+    }
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return QSP_OK;
@@ -766,7 +770,8 @@ int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* stream) {
 }
 
 int qsp_set_stream_parts(qsp_solver* s, int32_t parts) {
-    if (!s || parts < 0 || parts > 2) return fail(QSP_ERR_ARG, "qsp_set_stream_parts: parts must be 0 (auto), 1 or 2");
+    if (!s || parts < 0 || parts > SQP_MAX_PARTS)
+        return fail(QSP_ERR_ARG, "qsp_set_stream_parts: parts must be 0 (auto), 1 or 2");
     s->parts_req = parts;
     return QSP_OK;
 }

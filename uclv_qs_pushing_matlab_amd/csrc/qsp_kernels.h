@@ -58,19 +58,24 @@ struct SolveArgs {
 
 
 int lanes_per_instance(int N, int S);
-// Two-stream split of the SQP loop (SqpStreams::parts == 2): the instances are halved and
-// each half runs its own (sort, qp_step) sequence on its own stream, so the launch tail of
-// one half's QP overlaps the other half's work.  Results are bit-identical to the
-// single-stream loop (instances are independent).  Streams and events owned by the handle.
+// Multi-stream split of the SQP loop (SqpStreams::parts = P > 1): the instances are cut into
+// P parts and each part runs its own (sort, qp_step) sequence on its own stream (part 0 on
+// the solve's stream, part p on aux[p-1]), so the launch tail of one part's QP overlaps the
+// other parts' work.  Results are bit-identical to the single-stream loop (instances are
+// independent).  Streams and events owned by the handle.
+// Two parts at most: measured (scripts/parts_sweep.sh) three or four parts run slower than one
+// at every batch size (down to half the rate at B = 4 096) -- with GPU_MAX_HW_QUEUES = 4 the
+// extra streams share hardware queues, whose kernels then serialise across parts.
+constexpr int SQP_MAX_PARTS = 2;
 struct SqpStreams {
-    hipStream_t aux = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    int parts = 1;   // 1 or 2
+    hipStream_t aux[SQP_MAX_PARTS - 1] = {};
+    hipEvent_t fork = nullptr, join[SQP_MAX_PARTS - 1] = {};
+    int parts = 1;   // 1 .. SQP_MAX_PARTS
 };
 // ev (optional): 2*sqp_iters + 3 events recorded on `stream` at every kernel boundary
-// (prologue | sort, qp_step x sqp_iters | epilogue), for per-kernel timing.  With two parts
-// only ev[0], ev[1] (fork), ev[2K+1] (join) and ev[2K+2] are recorded: the SQP loop is timed
-// as a whole (qsp_get_kernel_times then reports K qp_step "launches" = SQP iterations).
+// (prologue | sort, qp_step x sqp_iters | epilogue), for per-kernel timing.  With several
+// parts only ev[0], ev[1] (fork), ev[2K+1] (join) and ev[2K+2] are recorded: the SQP loop is
+// timed as a whole (qsp_get_kernel_times then reports K qp_step "launches" = SQP iterations).
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr,
                       const SqpStreams* split = nullptr);
 int sqp_parts_auto(int B, int N, int S);

@@ -1680,14 +1680,16 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     return hipGetLastError();
 }
 
-// Two parts once each half still fills the 2 048 wave slots of the chip (2 waves/SIMD) about
-// four times over; below that a launch is mostly its own tail and the halves gain nothing.
-// Measured at the bench workload (B = 65 536, N = 20, 21 846 waves; scripts/two_streams.py
-// with one handle per part): 493k solves/s in one part, 513k in two, 514k in four.
+// Two parts once the batch fills the 2 048 wave slots of the chip (2 waves/SIMD) at least once;
+// below that the waves of one launch already run side by side and splitting only adds launches.
+// Measured (scripts/parts_sweep.sh, N = 20, K = 50, solves/s one part -> two parts): B = 4 096
+// (1 366 waves) 226k -> 218k; B = 8 192 323k -> 361k; B = 16 384 423k -> 505k; B = 32 768
+// 473k -> 509k; B = 65 536 491k -> 512k; N = 50, B = 16 384 (S = 2) 69.7k -> 74.8k; merit
+// SQP (max_iter 30) B = 65 536 619k -> 672k, and at N = 10 1.42M -> 1.65M.
 int sqp_parts_auto(int B, int N, int S) {
     const int G = 64 / lanes_per_instance(N, S);
     const long waves = ((long)B + G - 1) / G;
-    return waves >= 8 * 2048 ? 2 : 1;
+    return waves >= 2048 ? 2 : 1;
 }
 
 // One part's SQP loop on `stream`: (packing sort, QP [+ line search]) x sqp_iters over the
@@ -1709,9 +1711,14 @@ static hipError_t sqp_iteration(const SolveArgs& as, int S, bool sorted, int it,
 
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev, const SqpStreams* split) {
     const int G = 64 / lanes_per_instance(a.p.N, S);
-    // part boundary on a whole wave of the first part
-    const int h = (a.B / 2 / G) * G;
-    const bool two = split && split->aux && split->fork && split->join && split->parts == 2 && h > 0;
+    // parts of whole waves (the last part takes the remainder); at least one wave each
+    int P = split ? split->parts : 1;
+    if (P > SQP_MAX_PARTS) P = SQP_MAX_PARTS;
+    const int wtot = (a.B + G - 1) / G;
+    if (P > wtot) P = wtot;
+    for (int q = 1; q < P; ++q)
+        if (!split->aux[q - 1] || !split->join[q - 1] || !split->fork) P = 1;
+    const bool two = P > 1;
     const int K = a.p.sqp_iters;
     int ne = 0;
     auto mark = [&]() { return ev ? hipEventRecord(ev[ne++], stream) : hipSuccess; };
@@ -1730,26 +1737,31 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();
         if (e == hipSuccess)
-            e = hipMemsetAsync(a.whist, 0, (two ? 2 : 1) * 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
+            e = hipMemsetAsync(a.whist, 0, P * 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
     if (!two) {
         for (int it = 0; it < K && e == hipSuccess; ++it) e = sqp_iteration(as, S, sorted, it, stream, mark);
     } else {
-        // fork: the second half waits for the prologue, then both halves iterate independently
-        SolveArgs a0 = as, a1 = as;
-        a0.nI = h;
-        a1.i0 = h;
-        a1.nI = a.B - h;
-        if (sorted) a1.whist = a.whist + 4 * PACK_KEYS_MAX;
-        if (e == hipSuccess) e = hipEventRecord(split->fork, stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(split->aux, split->fork, 0);
-        for (int it = 0; it < K && e == hipSuccess; ++it) {
-            e = sqp_iteration(a0, S, sorted, it, stream, nomark);
-            if (e == hipSuccess) e = sqp_iteration(a1, S, sorted, it, split->aux, nomark);
+        // fork: the other parts wait for the prologue, then every part iterates independently
+        SolveArgs ap[SQP_MAX_PARTS];
+        hipStream_t sp[SQP_MAX_PARTS];
+        for (int q = 0; q < P; ++q) {
+            const int w0 = (int)((long)wtot * q / P), w1 = (int)((long)wtot * (q + 1) / P);
+            ap[q] = as;
+            ap[q].i0 = w0 * G;
+            ap[q].nI = (q + 1 < P ? w1 * G : a.B) - w0 * G;
+            if (sorted) ap[q].whist = a.whist + q * 4 * PACK_KEYS_MAX;
+            sp[q] = q == 0 ? stream : split->aux[q - 1];
         }
-        if (e == hipSuccess) e = hipEventRecord(split->join, split->aux);
-        if (e == hipSuccess) e = hipStreamWaitEvent(stream, split->join, 0);
+        if (e == hipSuccess) e = hipEventRecord(split->fork, stream);
+        for (int q = 1; q < P && e == hipSuccess; ++q) e = hipStreamWaitEvent(sp[q], split->fork, 0);
+        for (int it = 0; it < K && e == hipSuccess; ++it)
+            for (int q = 0; q < P && e == hipSuccess; ++q) e = sqp_iteration(ap[q], S, sorted, it, sp[q], nomark);
+        for (int q = 1; q < P && e == hipSuccess; ++q) {
+            e = hipEventRecord(split->join[q - 1], sp[q]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(stream, split->join[q - 1], 0);
+        }
         ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
     }
