@@ -79,6 +79,24 @@ def test_two_stream_parts_bit_identical(nlp_mode, B, K):
         np.testing.assert_array_equal(a, b)
 
 
+def test_stream_parts_auto_and_errors():
+    """auto: one part below one fill of the 2 048 wave slots (B = 4 096: 1 366 waves of three
+    instances), two from there on (B = 8 192); only 0, 1, 2 are accepted."""
+    from uclv_qs_pushing_matlab_amd._lib import QspError
+    s = _solver(4096, K=1)
+    assert s.stream_parts() == 1
+    s.close()
+    s = _solver(8192, K=1)
+    assert s.stream_parts() == 2
+    for bad in (-1, 3):
+        with pytest.raises(QspError, match="stream_parts"):
+            s.set_stream_parts(bad)
+    assert s.stream_parts() == 2
+    s.set_stream_parts(1)
+    assert s.stream_parts() == 1
+    s.close()
+
+
 def test_config4_batch_one_device():
     from bench import make_inputs
     B, N = 262144, 20
