@@ -1,10 +1,11 @@
 #!/bin/bash
-# Stream parts of the SQP loop (1..4) across batch sizes and NLP modes (no CPU leg); the data
-# behind sqp_parts_auto.  PARTS / BATCHES override the sweep.
+# Stream parts of the SQP loop across batch sizes and NLP modes (no CPU leg); the data behind
+# sqp_parts_auto.  PARTS / BATCHES override the sweep.  (3 and 4 parts, measured slower than one
+# part at every size before the library was capped at two -- DESIGN.md section 4.)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out/parts
-PARTS=${PARTS:-"1 2 3 4"}
+PARTS=${PARTS:-"1 2"}
 BATCHES=${BATCHES:-"4096 8192 16384 32768 65536"}
 run() {
   name=$1; shift
