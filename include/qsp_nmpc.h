@@ -176,7 +176,9 @@ int qsp_synchronize(qsp_solver* s);
  * HIP stream (forked from and joined back into the solve's stream), so that the tail of one
  * half's QP launch overlaps the other half's work.  Results are bit-identical either way.
  * parts: 0 = auto (two once the batch fills the GPU's wave slots), 1, or 2.  No acados
- * counterpart (an execution choice of the batched engine).  get: the count the next solve uses. */
+ * counterpart (an execution choice of the batched engine).  get: the count the next solve uses.
+ * Batches whose waves fit the GPU's SIMDs once (nlp_mode 0) run the whole SQP loop in one launch
+ * instead (one part; environment QSP_FUSED_LOOP=0/1 at qsp_create overrides the automatic choice). */
 int qsp_set_stream_parts(qsp_solver* s, int32_t parts);
 int qsp_get_stream_parts(qsp_solver* s, int32_t* parts);
 /* Per-kernel timing (acados' time_lin / time_qp split).  qsp_set_kernel_timing(s, n) pre-creates

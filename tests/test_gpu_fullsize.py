@@ -116,3 +116,26 @@ def test_config4_batch_one_device():
     us = small.controller_solve(x0[idx], 1)
     small.close()
     np.testing.assert_array_equal(us, u[idx])
+
+
+@pytest.mark.parametrize("B,S", [(2048, 1), (4096, 1), (2048, 2)])
+def test_fused_sqp_loop_bit_identical(monkeypatch, B, S):
+    """The whole SQP loop in one launch (sqp_loop_kernel, QSP_FUSED_LOOP=1) gives every lane
+    the same bits as the per-iteration launches (QSP_FUSED_LOOP=0)."""
+    from bench import make_inputs
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, K = 20, 50
+    x0, yref, yref_e, sid, traj = make_inputs(B, N, 20250303 + 3)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("QSP_FUSED_LOOP", fused)
+        s = OcpSolver(N=N, batch=B, sqp_iters=K, stages_per_lane=S)
+        s.set_shapes([make_shape(n) for n in NAMES])
+        s.set_reference_trajectory(traj)
+        s.set_shape_ids(sid)
+        u = s.controller_solve(x0, 1)
+        out[fused] = [u] + [s.get(f) for f in ("x", "u", "pi", "status", "sqp_iter", "qp_iter")]
+        s.close()
+    for a, b in zip(out["0"], out["1"]):
+        np.testing.assert_array_equal(a, b)

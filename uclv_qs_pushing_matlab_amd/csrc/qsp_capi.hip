@@ -71,11 +71,17 @@ struct qsp_solver {
     // two-stream SQP loop (launch_sqp): second stream, fork/join events, requested parts (0 = auto)
     SqpStreams split;
     int parts_req = 0;
+    int fused_req = -1;            // QSP_FUSED_LOOP (-1: auto)
 };
 
 // --------------------------------------------------------------- helpers
 static const SqpStreams* sqp_split(qsp_solver* s) {
     s->split.parts = s->parts_req > 0 ? s->parts_req : sqp_parts_auto(s->o.batch, s->o.N, s->S);
+    // the whole SQP loop in one launch: auto for batches below one fill of the wave slots
+    // when one part is in use; QSP_FUSED_LOOP=0/1 overrides (experiments, parity tests)
+    s->split.fused = s->fused_req >= 0 ? s->fused_req
+                                       : (s->split.parts == 1 && sqp_fused_auto(s->o.batch, s->o.N, s->S, s->o.nlp_mode));
+    if (s->split.fused) s->split.parts = 1;
     return &s->split;
 }
 
@@ -84,7 +90,7 @@ static hipEvent_t* take_kernel_events(qsp_solver* s) {
     const int per = 2 * s->o.sqp_iters + 3;
     if (s->kev.empty() || s->kev_used + per > (int)s->kev.size()) return nullptr;
     s->kev_solves.push_back(s->kev_used);
-    s->kev_split.push_back(sqp_split(s)->parts > 1 ? 1 : 0);
+    s->kev_split.push_back((sqp_split(s)->parts > 1 || s->split.fused) ? 1 : 0);
     hipEvent_t* e = s->kev.data() + s->kev_used;
     s->kev_used += per;
     return e;
@@ -369,6 +375,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (e == hipSuccess) e = hipMemsetAsync(s->PI.p, 0, B * N * 4 * 8, s->stream);
     // debug: every workspace byte starts as a NaN pattern, so a kernel that reads a word it
     // never wrote shows up as NaN (tests/test_gpu_errors.py)
+    if (const char* fl = std::getenv("QSP_FUSED_LOOP")) s->fused_req = (fl[0] == '1') ? 1 : (fl[0] == '0' ? 0 : -1);
     const char* pz = std::getenv("QSP_DEBUG_POISON");
     s->poison = pz && pz[0] == '1';
     if (s->poison) {

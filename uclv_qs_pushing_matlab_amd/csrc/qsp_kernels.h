@@ -71,6 +71,7 @@ struct SqpStreams {
     hipStream_t aux[SQP_MAX_PARTS - 1] = {};
     hipEvent_t fork = nullptr, join[SQP_MAX_PARTS - 1] = {};
     int parts = 1;   // 1 .. SQP_MAX_PARTS
+    int fused = 0;   // 1: the whole SQP loop in one launch (sqp_loop_kernel; small batches, nlp_mode 0)
 };
 // ev (optional): 2*sqp_iters + 3 events recorded on `stream` at every kernel boundary
 // (prologue | sort, qp_step x sqp_iters | epilogue), for per-kernel timing.  With several
@@ -79,6 +80,7 @@ struct SqpStreams {
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr,
                       const SqpStreams* split = nullptr);
 int sqp_parts_auto(int B, int N, int S);
+int sqp_fused_auto(int B, int N, int S, int nlp_mode);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
 hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
                                    hipStream_t stream);

@@ -1221,6 +1221,124 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     }
 }
 
+// Small batches (fewer waves than the chip's 2 048 wave slots), nlp_mode 0: the whole SQP loop
+// in one launch.  Every wave keeps its instances for all K iterations, so a solve costs the
+// slowest wave's own sum of IPM iterations instead of the sum over iterations of the slowest
+// wave of the batch (no packing sort, no grid-wide boundary between SQP iterations).  The
+// per-iteration arithmetic is qp_step_kernel<S, false, true>'s (same helpers, same order), so
+// the results are bit-identical to the per-iteration launches (tests/test_gpu_fullsize.py).
+template <int S>
+__global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArgs A) {
+    extern __shared__ double smem[];
+    const SolveParams& p = A.p;
+    const int N = p.N;
+    if (A.flags & QSP_FLAG_POISON) {
+        for (int f = 0; f < F_COUNT * S; ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
+    }
+    bool stopped = false;   // group-uniform: a failed QP stops the instance's SQP
+    for (int it = 0; it < p.sqp_iters; ++it) {
+        if (it > 0) __syncthreads();   // the neighbour lanes' X, U stores of the last iteration
+        // lane geometry and addresses re-derived every iteration from an opaque lane id: hoisted
+        // out of the loop they would stay live through the interior point (register budget)
+        int lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        Ctx c;
+        c.lane = lane;
+        c.N = N;
+        c.L = (N + S) / S;
+        const int G = 64 / c.L;
+        c.grp = c.lane / c.L;
+        c.lig = c.lane - c.grp * c.L;
+        c.base = c.grp * c.L;
+        c.gs.init(c.base, c.L);
+        const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        c.inst = wave * G + c.grp;
+        c.real = (c.grp < G) && (c.inst < A.nI);
+        const int iv = A.i0 + (c.real ? c.inst : A.nI - 1);
+        double* X = A.wX + (size_t)iv * (N + 1) * 4;
+        double* U = A.wU + (size_t)iv * N * 2;
+        if (it == 0) stopped = A.wdone[iv] != 0;
+        // a fresh register block per iteration: the factor walk writes K, Rn, kk in place under
+        // a lane mask, which would otherwise keep the last iteration's values live
+        Stage<S> st;
+        st.lds = smem + threadIdx.x;
+        const bool lin_live = c.real && !stopped;
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
+            const int kc = k <= N ? k : N;
+            const int ku = k < N ? k : N - 1;
+            if (kc < N && lin_live) {
+                const double xk[4] = {X[4 * kc], X[4 * kc + 1], X[4 * kc + 2], X[4 * kc + 3]};
+                const double uk[2] = {U[2 * kc], U[2 * kc + 1]};
+                Lin Ln;
+                rk4<true>(shape_of(A, iv), p.Ts, xk, uk, Ln);
+                const double* yr = A.yref + ((size_t)iv * N + kc) * 6;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) st.a[ls][q] = Ln.a[q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st.B[ls][q] = Ln.B[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.bb[ls][q] = Ln.xn[q] - X[4 * (kc + 1) + q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.g[ls][q] = p.tau * p.W[q] * (xk[q] - yr[q]);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) st.g[ls][4 + q] = p.tau * p.W[4 + q] * (uk[q] - yr[4 + q]);
+            } else {
+                const double* ye = A.yref_e + (size_t)iv * 4;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) st.a[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st.B[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.bb[ls][q] = 0.0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st.g[ls][q] = p.We[q] * (X[4 * N + q] - ye[q]);
+                st.g[ls][4] = 0.0;
+                st.g[ls][5] = 0.0;
+            }
+            st.v(ls, 0) = X[4 * kc + 3];
+            st.v(ls, 1) = U[2 * ku];
+            st.v(ls, 2) = U[2 * ku + 1];
+        }
+        double dx0[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
+        const bool skip = stopped || !c.real;
+        const int nit = qp_ipm<S>(c, p, st, dx0, skip);
+        qp_rollout<S>(c, st, dx0);
+        double bad = 0.0;
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
+            bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
+        }
+        const bool failed = !skip && group_max(bad, c.gs) > 0.0;
+        if (failed && c.real && c.lig == 0) {
+            A.wdone[iv] = 2;
+            A.sqp_iter[iv] = it;
+        }
+        qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real && !skip && !failed,
+                            (A.flags & QSP_FLAG_SHIFT) != 0);
+        if (c.real && !skip && !failed) {
+#pragma unroll
+            for (int ls = 0; ls < S; ++ls) {
+                const int k = kof<S>(c, ls);
+                if (k <= N)
+                    for (int q = 0; q < 4; ++q) X[4 * k + q] += st.dxs(ls, q);
+                if (k < N) {
+                    U[2 * k] += st.du(ls, 0);
+                    U[2 * k + 1] += st.du(ls, 1);
+                }
+                if (k == 0) A.qp_iter[iv] += nit;
+            }
+        }
+        stopped = stopped || failed;
+    }
+}
+
 // Counting sort of the instances by their packing key (pack_key) in one pass over the
 // instances: the histogram of the keys was accumulated by the QP launch itself (whist,
 // parity q); every block forms the exclusive prefix of the histogram (a block-wide scan),
@@ -1655,6 +1773,30 @@ static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream)
     return hipGetLastError();
 }
 
+template <int S>
+static hipError_t launch_sqp_loop(const SolveArgs& a, hipStream_t stream) {
+    const int L = (a.p.N + S) / S;
+    const int G = 64 / L;
+    const int waves = (a.nI + G - 1) / G;
+    const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t e = lds_attr_once((const void*)sqp_loop_kernel<S>, lds_bytes<S>(), attr);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((sqp_loop_kernel<S>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a);
+    return hipGetLastError();
+}
+
+// sqp_loop_kernel keeps more state live across its SQP loop than qp_step_kernel and runs at
+// 1 wave/SIMD (256 VGPRs + AGPRs), so it pays only while its waves fit the 1 024 SIMDs in one
+// round.  Measured (scripts/fused_sweep.sh, N = 20, K = 50, S = 1, solves/s per-iteration
+// launches -> fused): B = 1 024 58.7k -> 76.5k; 2 048 115k -> 123k; 3 072 (1 024 waves) 173k ->
+// 224k; 4 096 (1 366 waves, two rounds) 227k -> 169k.
+int sqp_fused_auto(int B, int N, int S, int nlp_mode) {
+    const int G = 64 / lanes_per_instance(N, S);
+    const long waves = ((long)B + G - 1) / G;
+    return (nlp_mode == 0 && waves <= 1024) ? 1 : 0;
+}
+
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
         case 1: return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
@@ -1718,6 +1860,8 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (P > wtot) P = wtot;
     for (int q = 1; q < P; ++q)
         if (!split->aux[q - 1] || !split->join[q - 1] || !split->fork) P = 1;
+    const bool fused = split && split->fused && a.p.nlp_mode == 0 && a.wdone && (S == 1 || S == 2);
+    if (fused) P = 1;
     const bool two = P > 1;
     const int K = a.p.sqp_iters;
     int ne = 0;
@@ -1728,7 +1872,8 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
-    const bool sorted = a.wperm && a.wnit && a.whist && (a.p.qp_iters + 1) * (a.p.qp_iters + 1) <= PACK_KEYS_MAX;
+    const bool sorted = !fused && a.wperm && a.wnit && a.whist &&
+                        (a.p.qp_iters + 1) * (a.p.qp_iters + 1) <= PACK_KEYS_MAX;
     SolveArgs as = a;
     as.i0 = 0;
     as.nI = a.B;
@@ -1740,7 +1885,11 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
             e = hipMemsetAsync(a.whist, 0, P * 4 * PACK_KEYS_MAX * sizeof(int32_t), stream);
     }
     if (e == hipSuccess) e = mark();
-    if (!two) {
+    if (fused) {
+        if (e == hipSuccess) e = S == 1 ? launch_sqp_loop<1>(as, stream) : launch_sqp_loop<2>(as, stream);
+        ne = 2 * K + 1;
+        if (e == hipSuccess) e = mark();
+    } else if (!two) {
         for (int it = 0; it < K && e == hipSuccess; ++it) e = sqp_iteration(as, S, sorted, it, stream, mark);
     } else {
         // fork: the other parts wait for the prologue, then every part iterates independently
