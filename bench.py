@@ -104,7 +104,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="lanes per GPU")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--sqp-iters", type=int, default=50)
-    ap.add_argument("--qp-iters", type=int, default=20)
+    ap.add_argument("--qp-iters", type=int, default=50)
     ap.add_argument("--stages-per-lane", type=int, default=0)
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
                     help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")

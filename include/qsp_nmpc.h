@@ -44,6 +44,8 @@ extern "C" {
 #define QSP_STATUS_SUCCESS 0
 #define QSP_STATUS_NAN 1
 #define QSP_STATUS_MAXITER 2      /* QSP_NLP_SQP_MERIT: tolerances not met within sqp_iters */
+#define QSP_STATUS_QP_FAIL 4      /* acados ACADOS_QP_FAILURE: infeasible QP (stage0_s_bound with x0's s
+                                     outside [lh_s, uh_s]); the instance does not iterate */
 
 #define QSP_NLP_SQP_RTI_FIXED 0   /* K full Gauss-Newton steps: the BASELINE metric */
 #define QSP_NLP_SQP_MERIT 1       /* acados 'SQP' + 'merit_backtracking' with KKT tolerances
@@ -69,6 +71,13 @@ typedef struct {
     double tol_stat, tol_eq, tol_ineq, tol_comp;
     double ls_alpha_min, ls_alpha_red, ls_eps;
     double res_stop;          /* interior point stops when mu < mu_stop AND the bound residual < res_stop */
+    /* ... AND (HPIPM's other two exit residuals, ocp_qp_ipm res_g / res_b) the stationarity and
+     * equality residuals of the IPM iterate are below these (tracked exactly: each Newton step
+     * scales them by 1 - alpha); qp_iters (default 50, acados qp_solver_iter_max) caps it */
+    double qp_tol_stat, qp_tol_eq;
+    int32_t stage0_s_bound;   /* 1 (default): the s bound of h also applies at stage 0 (acados bgh on
+                                 stages 0..N-1, NMPC_controller.m:237,251-252); 0: stages 1..N-1 */
+    int32_t pad2_;
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */
@@ -142,6 +151,9 @@ int qsp_get_cost(qsp_solver* s, double* cost /* B */);
 int qsp_get_status(qsp_solver* s, int32_t* status /* B */);
 int qsp_get_sqp_iter(qsp_solver* s, int32_t* sqp_iter /* B */);
 int qsp_get_qp_iter(qsp_solver* s, int32_t* qp_iter /* B, summed over the SQP iterations */);
+/* QPs of the last solve that stopped at the iteration cap qp_iters instead of meeting the stop
+ * test (their last iterate is used, as HPIPM's at iter_max): B counts */
+int qsp_get_qp_capped(qsp_solver* s, int32_t* capped /* B */);
 int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
 
 /* --------------------------------------- NMPC_controller.solve(x0, index_time) */
@@ -201,10 +213,12 @@ int qsp_eval_rk4(qsp_solver* s, int32_t n, const int32_t* shape_id, double h, co
 int qsp_eval_vbound(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* sval, double* vb);
 /* Batched LQ-QP (interior point) with per-stage data; H and bound widths must be equal on
  * every stage (as in the OCP).  H: nb x (6N+4) diag, g: nb x (6N+4), lo/hi: nb x N x 3,
- * stage-0 s bound inactive. */
+ * stage-0 s bound as the handle's stage0_s_bound.  qp_status (optional, nb): 0 the stop test
+ * was met, 1 non-finite solution, 2 stopped at the iteration cap, 3 infeasible (the fixed
+ * stage-0 s = dx0's outside its bounds). */
 int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, const double* b, const double* H,
                  const double* g, const double* lo, const double* hi, const double* dx0, double* dx, double* du,
-                 double* pi, double* lam, int32_t* iters);
+                 double* pi, double* lam, int32_t* iters, int32_t* qp_status);
 
 #ifdef __cplusplus
 }

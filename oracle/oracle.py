@@ -42,16 +42,19 @@ class Opts(C.Structure):
         ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
         ("res_stop", C.c_double),
+        ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
     ]
 
 
-def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
+def make_opts(N=20, sqp_iters=50, qp_iters=50, Ts=0.05, tau=None,
               W=(1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3), We=(2e5, 2e5, 20.0, 0.0),
               lh=(-0.06, 0.0, -0.05), uh=(0.011, 0.03, 0.05),
               mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
-              u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4):
+              u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
+              qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1):
     o = Opts()
-    o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, 0
+    o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, int(stage0_s_bound)
+    o.qp_tol_stat, o.qp_tol_eq = qp_tol_stat, qp_tol_eq
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W
@@ -144,9 +147,10 @@ class Oracle:
         pi = np.zeros((nb, N, 4))
         lam = np.zeros((nb, N, 6))
         iters = np.zeros(nb, np.int32)
+        qst = np.zeros(nb, np.int32)
         r = self.L.or_qp_batch(C.byref(opts), C.c_int32(nb), *[_p(a) for a in arrs], _p(act), _p(dx0),
-                               _p(dx), _p(du), _p(pi), _p(lam), _p(iters))
-        return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters, fail=r)
+                               _p(dx), _p(du), _p(pi), _p(lam), _p(iters), _p(qst))
+        return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters, fail=r, qp_status=qst)
 
     def ocp_solve(self, opts, x0, yref, yref_e, X=None, U=None, PI=None, shape_id=None, nthreads=0):
         N = opts.N
@@ -163,10 +167,11 @@ class Oracle:
         iters = np.zeros(nb, np.int32)
         qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
+        capped = np.zeros(nb, np.int32)
         self.L.or_ocp_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
                             _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                            C.c_int(nthreads))
-        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
+                            C.c_int(nthreads), _p(capped))
+        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
 
     def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0):
         """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place."""
@@ -181,11 +186,12 @@ class Oracle:
         iters = np.zeros(nb, np.int32)
         qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
+        capped = np.zeros(nb, np.int32)
         self.L.or_controller_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
                                    C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]),
                                    _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                                   C.c_int(nthreads))
-        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
+                                   C.c_int(nthreads), _p(capped))
+        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
 
     @staticmethod
     def new_warm(nb, N):

@@ -58,7 +58,9 @@ typedef struct {
     int32_t N;          /* horizon (param_scheme_N) */
     int32_t sqp_iters;  /* K full Gauss-Newton steps */
     int32_t qp_iters;   /* Mehrotra iterations per QP */
-    int32_t stage0_s_bound; /* reserved (0: s bound skipped at stage 0, x0 is fixed) */
+    int32_t stage0_s_bound; /* 1: the s bound of h also applies at stage 0 (acados-recall: bgh at
+                               stage 0, NMPC_controller.m:237,251-252); s_0 is fixed by x0, so an
+                               x0 with s outside [lh_s, uh_s] makes every QP infeasible */
     double Ts;          /* h = T/N */
     double tau;         /* stage-cost scaling (acados: Ts) */
     double W[6];        /* diag(blkdiag(W_x, W_u))   (NMPC_controller.m:157, main.m:82-86) */
@@ -78,6 +80,12 @@ typedef struct {
     double tol_stat, tol_eq, tol_ineq, tol_comp;
     double ls_alpha_min, ls_alpha_red, ls_eps;
     double res_stop;    /* per-QP early exit also needs the bound residual below res_stop */
+    /* HPIPM-style QP termination (ocp_qp_ipm: res_g, res_b next to res_d = res_stop and
+     * res_m = mu_stop): the stationarity and equality residuals of the IPM iterate.  Both are
+     * linear in the iterate and every Newton step solves them exactly, so each update scales
+     * them by (1 - alpha): tracked as r_0 * prod(1 - alpha) from the start point (z = 0, pi = 0,
+     * lam = mu0 / t), like the bound residual. */
+    double qp_tol_stat, qp_tol_eq;
 } or_opts;
 
 /* ================================================================ dual numbers */
@@ -414,7 +422,9 @@ static inline double bnd_val(const double *dx, const double *du, int k, int j)
     return j == 0 ? dx[4 * k + 3] : du[2 * k + (j - 1)];
 }
 
-/* Mehrotra predictor-corrector IPM.  Returns 0 on success, 1 on NaN. */
+/* Mehrotra predictor-corrector IPM.  Returns 0 (stop test met), 1 (non-finite solution),
+ * 2 (iteration cap reached first: the last iterate is returned, as HPIPM at iter_max),
+ * 3 (infeasible: a fixed bounded component, the stage-0 s = x0's s, lies outside its bounds). */
 static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, double *work, int *nit_out)
 {
     int N = qp->N;
@@ -441,14 +451,38 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         }
     for (int k = 0; k < N; ++k) { sol->du[2 * k] = 0.0; sol->du[2 * k + 1] = 0.0; }
     static const int comp[3] = {3, 4, 5};
+    /* the stage-0 s is fixed (dx_0 = dx0): its bound is a feasibility check, not a variable */
+    int infeasible = 0;
+    if (qp->act[0]) {
+        double v = qp->dx0[3];
+        if (v < qp->lo[0] || v > qp->hi[0]) infeasible = 1;
+    }
+    /* start-point residuals of the stop test (z = 0, pi = 0): stationarity g + C' lam,
+     * equality dx0 and the defects b */
+    double rg0 = 0.0, rb0 = 0.0;
+    for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < 6; ++i) {
+            double r = qp->g[6 * k + i];
+            int j = i == 3 ? 0 : (i >= 4 ? i - 3 : -1);
+            if (j >= 0 && qp->act[k * 3 + j]) r += lam[(k * 3 + j) * 2 + 1] - lam[(k * 3 + j) * 2 + 0];
+            if (fabs(r) > rg0) rg0 = fabs(r);
+        }
+        for (int i = 0; i < 4; ++i) if (fabs(qp->b[4 * k + i]) > rb0) rb0 = fabs(qp->b[4 * k + i]);
+    }
+    for (int i = 0; i < 4; ++i) {
+        if (fabs(qp->g[6 * N + i]) > rg0) rg0 = fabs(qp->g[6 * N + i]);
+        if (fabs(qp->dx0[i]) > rb0) rb0 = fabs(qp->dx0[i]);
+    }
 
-    int nit = 0;
-    for (int it = 0; it < o->qp_iters; ++it) {
+    int nit = 0, converged = 0;
+    for (int it = 0; it <= o->qp_iters && !infeasible; ++it) {
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
         mu /= (double)m;
-        /* stop on complementarity AND primal (bound) feasibility (HPIPM checks both) */
-        if (!(mu >= o->mu_stop) && !(r0 * rscale >= o->res_stop)) break;
+        /* HPIPM's four exit residuals: complementarity, bound, stationarity, equality */
+        if (!(mu >= o->mu_stop) && !(r0 * rscale >= o->res_stop) && !(rg0 * rscale >= o->qp_tol_stat) &&
+            !(rb0 * rscale >= o->qp_tol_eq)) { converged = 1; break; }
+        if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
@@ -546,7 +580,8 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     }
     for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(sol->dx[q])) return 1;
     for (int q = 0; q < 2 * N; ++q) if (!isfinite(sol->du[q])) return 1;
-    return 0;
+    if (infeasible) return 3;
+    return converged ? 0 : 2;
 }
 
 /* ================================================================ SQP */
@@ -560,6 +595,7 @@ typedef struct {
     double work[OR_MAX_N * 40 + 64];
     or_fact F;
     int qp_total;
+    int qp_capped;   /* QPs of this solve stopped by the iteration cap */
 } or_ws;
 
 static double ocp_cost(const or_opts *o, int N, const double *X, const double *U, const double *yref, const double *yref_e)
@@ -588,7 +624,7 @@ static double merit_eval(const or_shape *sh, const or_opts *o, const double *X, 
         rk4_sens(sh, o->Ts, X + 4 * k, U + 2 * k, xn, A, B);
         for (int i = 0; i < 4; ++i) phi += nu[4 * k + i] * fabs(xn[i] - X[4 * (k + 1) + i]);
         double v[3] = {X[4 * k + 3], U[2 * k], U[2 * k + 1]};
-        for (int j = (k == 0 ? 1 : 0); j < 3; ++j) {
+        for (int j = (k == 0 && !o->stage0_s_bound ? 1 : 0); j < 3; ++j) {
             double vl = o->lh[j] - v[j], vh = v[j] - o->uh[j];
             if (vl > 0) phi += eta[(3 * k + j) * 2 + 0] * vl;
             if (vh > 0) phi += eta[(3 * k + j) * 2 + 1] * vh;
@@ -621,6 +657,13 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
     memset(eta, 0, sizeof(double) * 6 * N);
     int it;
     if (o->nlp_mode == 1) status = 2;
+    /* stage-0 s bound: s_0 = x0's s is fixed in every QP; outside [lh_s, uh_s] all of them are
+     * infeasible and the solve stops before its first iteration (status 4, ACADOS_QP_FAILURE) */
+    if (o->stage0_s_bound && !(x0[3] >= o->lh[0] && x0[3] <= o->uh[0])) {
+        if (iters) *iters = 0;
+        if (lam_out) memset(lam_out, 0, sizeof(double) * 6 * N);
+        return 4;
+    }
     for (it = 0; it < o->sqp_iters; ++it) {
         for (int k = 0; k < N; ++k) {
             double xn[4];
@@ -638,7 +681,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
             for (int j = 0; j < 3; ++j) {
                 ws->lo[3 * k + j] = o->lh[j] - v[j];
                 ws->hi[3 * k + j] = o->uh[j] - v[j];
-                ws->act[3 * k + j] = (j == 0 && k == 0) ? 0 : 1;
+                ws->act[3 * k + j] = (j == 0 && k == 0) ? (uint8_t)(o->stage0_s_bound != 0) : 1;
             }
         }
         for (int i = 0; i < 4; ++i) {
@@ -666,7 +709,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                     }
                 }
                 for (int i = 0; i < 4; ++i) if (fabs(ws->b[4 * k + i]) > r_eq) r_eq = fabs(ws->b[4 * k + i]);
-                for (int j = (k == 0 ? 1 : 0); j < 3; ++j) {
+                for (int j = (k == 0 && !o->stage0_s_bound ? 1 : 0); j < 3; ++j) {
                     double sl = -ws->lo[3 * k + j], sh_ = ws->hi[3 * k + j];
                     if (-sl > r_ineq) r_ineq = -sl;
                     if (-sh_ > r_ineq) r_ineq = -sh_;
@@ -685,8 +728,12 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
             }
         }
         int nit = 0;
-        if (qp_solve(&qp, o, &sol, &ws->F, ws->work, &nit)) { status = 1; ws->qp_total += nit; break; }
+        const int qst = qp_solve(&qp, o, &sol, &ws->F, ws->work, &nit);
         ws->qp_total += nit;
+        if (qst == 2) ws->qp_capped++;
+        /* non-finite QP solution: status 1; infeasible QP: status 4 (acados ACADOS_QP_FAILURE);
+         * either way the SQP stops with its last finite iterate */
+        if (qst == 1 || qst == 3) { status = qst == 1 ? 1 : 4; break; }
         double alpha = 1.0;
         if (o->nlp_mode == 1) {
             /* merit weights (acados: max(|mult|, (weight + |mult|)/2)) */
@@ -707,7 +754,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 for (int i = 0; i < 4; ++i) dphi += ws->g[6 * k + i] * ws->dx[4 * k + i];
                 for (int i = 0; i < 2; ++i) dphi += ws->g[6 * k + 4 + i] * ws->du[2 * k + i];
                 for (int i = 0; i < 4; ++i) dphi -= nu[4 * k + i] * fabs(ws->b[4 * k + i]);
-                for (int j = (k == 0 ? 1 : 0); j < 3; ++j) {
+                for (int j = (k == 0 && !o->stage0_s_bound ? 1 : 0); j < 3; ++j) {
                     if (ws->lo[3 * k + j] > 0) dphi -= eta[(3 * k + j) * 2 + 0] * ws->lo[3 * k + j];
                     if (ws->hi[3 * k + j] < 0) dphi -= eta[(3 * k + j) * 2 + 1] * (-ws->hi[3 * k + j]);
                 }
@@ -803,7 +850,8 @@ int or_vbound(const int32_t *n_ctrl, const double *ctrl, const double *knots, co
  * Outputs dx ((N+1)x4), du (N x 2), pi (N x 4), lam (N x 6). */
 int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, const double *b,
                 const double *H, const double *g, const double *lo, const double *hi, const uint8_t *act,
-                const double *dx0, double *dx, double *du, double *pi, double *lam, int32_t *iters)
+                const double *dx0, double *dx, double *du, double *pi, double *lam, int32_t *iters,
+                int32_t *qp_status /* optional: 0 converged, 1 non-finite, 2 capped, 3 infeasible */)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -821,7 +869,9 @@ int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, 
             memcpy(qp.dx0, dx0 + 4 * i, sizeof qp.dx0);
             or_qp_sol sol = {dx + (size_t)i * 4 * (N + 1), du + (size_t)i * 2 * N, pi + (size_t)i * 4 * N,
                              lam + (size_t)i * 6 * N, ws->t};
-            if (qp_solve(&qp, o, &sol, &ws->F, ws->work, iters ? iters + i : NULL)) {
+            const int st = qp_solve(&qp, o, &sol, &ws->F, ws->work, iters ? iters + i : NULL);
+            if (qp_status) qp_status[i] = st;
+            if (st == 1) {
                 #pragma omp atomic write
                 fail = 1;
             }
@@ -838,7 +888,7 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
                  int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
                  const double *x0, const double *yref, const double *yref_e,
                  double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
-                 double *cost, int nthreads)
+                 double *cost, int nthreads, int32_t *qp_capped)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -854,8 +904,10 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
             double *Xi = X + (size_t)i * 4 * (N + 1), *Ui = U + (size_t)i * 2 * N, *Pi = PI + (size_t)i * 4 * N;
             const double *yr = yref + (size_t)i * 6 * N, *ye = yref_e + (size_t)i * 4;
             ws->qp_total = 0;
+            ws->qp_capped = 0;
             status[i] = sqp_solve(&sh, o, x0 + 4 * i, yr, ye, Xi, Ui, Pi, lam ? lam + (size_t)i * 6 * N : NULL, iters ? iters + i : NULL, ws);
             if (qp_iter) qp_iter[i] = ws->qp_total;
+            if (qp_capped) qp_capped[i] = ws->qp_capped;
             cost[i] = ocp_cost(o, N, Xi, Ui, yr, ye);
         }
         free(ws);
@@ -872,7 +924,8 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                         int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
                         const double *x0_in, const double *traj, int32_t T, const int32_t *index_time,
                         double *Xw, double *Uw, double *PIw, uint8_t *warm_valid,
-                        double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads)
+                        double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads,
+                        int32_t *qp_capped)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -927,8 +980,10 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
             }
             /* :389 solve */
             ws->qp_total = 0;
+            ws->qp_capped = 0;
             status[i] = sqp_solve(&sh, o, x0, yref, ye, X, U, PI, NULL, iters ? iters + i : NULL, ws);
             if (qp_iter) qp_iter[i] = ws->qp_total;
+            if (qp_capped) qp_capped[i] = ws->qp_capped;
             cost[i] = ocp_cost(o, N, X, U, yref, ye);
             u0[2 * i] = U[0]; u0[2 * i + 1] = U[1];
             /* :397-399 shift (duplicate last column) */

@@ -25,7 +25,7 @@ def build_qp(oracle, opts, X, U, yref, yref_e, x0, shape_id=None):
         v = np.stack([X[:, k, 3], U[:, k, 0], U[:, k, 1]], 1)
         lo[:, k] = np.array(opts.lh[:]) - v
         hi[:, k] = np.array(opts.uh[:]) - v
-    act[:, 0, 0] = 0
+    act[:, 0, 0] = 1 if opts.stage0_s_bound else 0
     H[:, 6 * N:] = We
     g[:, 6 * N:] = We * (X[:, N] - yref_e)
     dx0 = x0 - X[:, 0]

@@ -24,8 +24,10 @@ def test_closed_loop_config1_golden(N):
     s.set_reference_trajectory(straight_traj())
     r = s.closed_loop(np.zeros(4), 20)
     s.close()
+    # 20 closed-loop steps of K = 5 full SQP steps amplify rounding (two formulations of the
+    # spline and the Jacobian): 1e-8 on u0 and x (BASELINE asks 1e-6)
     for lane in range(4):      # identical lanes give identical trajectories
-        np.testing.assert_allclose(r["U"][lane], gold["u0"], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(r["U"][lane], gold["u0"], rtol=0, atol=1e-8)
         np.testing.assert_allclose(r["X"][lane, -1], gold["x_final"], atol=1e-9)
     assert np.all(r["status"] == 0)
 
@@ -50,15 +52,18 @@ def test_closed_loop_batched_noise(oracle):
     def oracle_loop(xs):
         warm = oracle.new_warm(nb, N)
         x = xs + noise[0]
-        X, U = [x], []
+        X, U, ST = [x], [], []
         for t in range(T):
             ro = oracle.controller_solve(op, x, traj, 1 + t, warm, shape_id=sid)
             f, _ = oracle.dynamics(x, ro["u0"], sid)
             x = x + 0.05 * f + (noise[t + 1] if t + 1 < T else 0.0)
             X.append(x)
             U.append(ro["u0"])
+            ST.append(ro["status"])
+        oracle_loop.status = np.stack(ST, 1)
         return np.stack(X, 1), np.stack(U, 1)
     Xo, Uo = oracle_loop(x0)
+    So = oracle_loop.status
     # closed-loop stable lanes: the oracle's own trace does not move under 1e-13 perturbations
     stable = np.ones(nb, bool)
     for f in (1e-13, -1e-13):
@@ -69,7 +74,9 @@ def test_closed_loop_batched_noise(oracle):
     dx = np.abs(r["X"] - Xo).max(axis=(1, 2))
     assert du[stable].max() < 1e-6, np.sort(du[stable])[-4:]
     assert dx[stable].max() < 1e-8, np.sort(dx[stable])[-4:]
-    assert np.all(r["status"] == 0)
+    # a lane whose s leaves [lh_s, uh_s] gets an infeasible stage-0 bound: status 4, as the oracle
+    assert set(np.unique(r["status"])) <= {0, 4}
+    assert np.all(r["status"][stable] == So[stable])
 
 
 def test_closed_loop_config1_rti_full():

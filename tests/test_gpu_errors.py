@@ -73,10 +73,14 @@ def test_device_shape_ids_are_clamped():
     assert np.all(status.cpu().numpy() == 0)
 
 
-@pytest.mark.parametrize("mode,S", [("SQP_RTI", 1), ("SQP_RTI", 2), ("SQP", 1)])
-def test_no_uninitialised_reads(monkeypatch, mode, S):
+@pytest.mark.parametrize("mode,S,fused", [("SQP_RTI", 1, "0"), ("SQP_RTI", 1, "1"), ("SQP_RTI", 2, "0"),
+                                          ("SQP_RTI", 2, "1"), ("SQP", 1, "0")])
+def test_no_uninitialised_reads(monkeypatch, mode, S, fused):
     """QSP_DEBUG_POISON=1 fills every workspace buffer and the QP kernels' LDS with NaN
-    before use: a kernel that reads a word it never wrote would change the result."""
+    before use (the fused SQP-loop kernel re-poisons its LDS at every SQP iteration): a kernel
+    that reads a word it never wrote would change the result.  Both the per-iteration QP
+    kernel (QSP_FUSED_LOOP=0, which every bench-size batch uses) and the fused loop."""
+    monkeypatch.setenv("QSP_FUSED_LOOP", fused)
     from conftest import config2_x0
     from uclv_qs_pushing_matlab_amd.objects import make_shape
     from uclv_qs_pushing_matlab_amd.solver import OcpSolver
@@ -99,3 +103,65 @@ def test_no_uninitialised_reads(monkeypatch, mode, S):
     for a, b in zip(clean, poisoned):
         np.testing.assert_array_equal(a, b)
     assert np.all(clean[2] == (0 if mode == "SQP_RTI" else clean[2]))
+
+
+@pytest.mark.parametrize("mode,B", [("SQP_RTI", 8192), ("SQP", 8192), ("SQP_RTI", 96)])
+def test_qp_iters_beyond_packing_levels(mode, B):
+    """qp_iters > 31 (acados' default cap is 50): the wave-packing keys clamp their levels at 31,
+    the packing stays on (per-iteration launches, two stream parts at B = 8 192), and every lane
+    gets the bits it gets when solved in a batch of its own kind (instances are independent)."""
+    from conftest import config2_x0
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N = 20
+    x0 = config2_x0(B, 91)
+    sid = np.arange(B) % 4
+    names = ("santal", "balea", "montana", "pulirapid")
+
+    def run(n, qp_iters):
+        s = OcpSolver(N=N, batch=n, sqp_iters=8, qp_iters=qp_iters, nlp_solver_type=mode)
+        s.set_shapes([make_shape(q) for q in names], shape_id=sid[:n])
+        s.set_reference_trajectory(straight_traj())
+        u = s.controller_solve(x0[:n], 1)
+        out = (u, s.get("status"), s.get("qp_iter"), s.get("qp_capped"), s.stream_parts())
+        s.close()
+        return out
+    u, st, qi, cap, parts = run(B, 40)
+    assert np.all(np.isfinite(u)) and set(np.unique(st)) <= {0, 2}
+    u_s, st_s, qi_s, cap_s, _ = run(64, 40)
+    np.testing.assert_array_equal(u[:64], u_s)
+    np.testing.assert_array_equal(qi[:64], qi_s)
+    np.testing.assert_array_equal(cap[:64], cap_s)
+    if B >= 8192:
+        assert parts == 2
+
+
+def test_stage0_s_bound_infeasible(oracle):
+    """stage0_s_bound (default on, acados bgh at stage 0): an x0 whose s lies outside
+    [lh_s, uh_s] = [-0.06, 0.011] makes every QP infeasible -> status 4 (ACADOS_QP_FAILURE),
+    sqp_iter 0, the other lanes unaffected; with the option off the lane solves (status 0)."""
+    from conftest import config2_x0
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, B, K = 20, 8, 5
+    x0 = config2_x0(B, 3)
+    x0[2, 3] = 0.05          # above uh_s
+    x0[5, 3] = -0.07         # below lh_s
+    traj = straight_traj()
+    res = {}
+    for on in (True, False):
+        s = OcpSolver(N=N, batch=B, sqp_iters=K, stage0_s_bound=on)
+        s.set_shapes([make_shape("santal")])
+        s.set_reference_trajectory(traj)
+        u = s.controller_solve(x0, 1)
+        res[on] = (u, s.get("status"), s.get("sqp_iter"))
+        s.close()
+        r = oracle.controller_solve(make_opts(N=N, sqp_iters=K, stage0_s_bound=int(on)), x0, traj, 1,
+                                    oracle.new_warm(B, N))
+        np.testing.assert_array_equal(res[on][1], r["status"])
+        np.testing.assert_array_equal(res[on][2], r["iters"])
+        np.testing.assert_allclose(u, r["u0"], rtol=0, atol=1e-6)
+    u, st, it = res[True]
+    assert list(np.where(st != 0)[0]) == [2, 5] and np.all(st[[2, 5]] == 4) and np.all(it[[2, 5]] == 0)
+    assert np.all(res[False][1] == 0)

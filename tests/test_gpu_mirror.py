@@ -56,7 +56,7 @@ def test_controller_mirror_config1_golden(N):
     x = np.zeros(4)
     for i in range(1, 21):
         u = ctrl.solve(x, i)[0]
-        np.testing.assert_allclose(u, gold["u0"][i - 1], rtol=0, atol=1e-9, err_msg=f"step {i}")
+        np.testing.assert_allclose(u, gold["u0"][i - 1], rtol=0, atol=1e-8, err_msg=f"step {i}")
         x = x + 0.05 * plant.evalModelVariableShape(x[None], u[None])[0]
     np.testing.assert_allclose(x, gold["x_final"], atol=1e-9)
     assert len(ctrl.cost_function_vect) == 20

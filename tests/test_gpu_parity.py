@@ -100,16 +100,28 @@ def _iterate(oracle, op, nb, seed, sqp_iters):
 
 
 def test_qp_matches_oracle(gpu, oracle):
+    """Every QP that met the stop test on both sides agrees to 1e-7 (relative to the u range),
+    except the ill-conditioned ones: the oracle's own solution moves by > 1e-8 when the gradient
+    is perturbed by 1e-13 relative (u_t carries only tau W_u = 5e-5 of curvature: DESIGN.md
+    section 2).  Status codes (0 stop test met, 2 cap, 3 infeasible) agree on every QP."""
     from oracle.oracle import make_opts
     op = make_opts(N=20)
     x0, yref, yref_e, X, U = _iterate(oracle, op, 64, 7, 3)
     A, B, b, H, g, lo, hi, act, dx0 = build_qp(oracle, op, X, U, yref, yref_e, x0)
     ref = oracle.qp(op, A, B, b, H, g, lo, hi, act, dx0)
     out = gpu.qp_solve(A, B, b, H, g, lo, hi, dx0)
+    np.testing.assert_array_equal(out["qp_status"], ref["qp_status"])
+    sens = np.zeros(len(x0), bool)
+    for f in (1e-13, -1e-13):
+        rp = oracle.qp(op, A, B, b, H, g * (1 + f), lo, hi, act, dx0)
+        sens |= np.abs(rp["du"] - ref["du"]).max(axis=(1, 2)) > 1e-8
     scale_u = 0.05
     err = np.abs(out["du"] - ref["du"]).max(axis=(1, 2)) / scale_u
+    conv = (ref["qp_status"] == 0) & (out["qp_status"] == 0)
+    assert conv.mean() > 0.95
+    assert sens.mean() < 0.2, sens.mean()
     assert np.median(err) < 1e-8, np.sort(err)[-5:]
-    assert np.mean(err < 1e-6) > 0.9, np.sort(err)[-5:]
+    assert err[conv & ~sens].max() < 1e-7, np.sort(err[conv & ~sens])[-5:]
 
 
 def test_ocp_solve_config2_parity(gpu, oracle):

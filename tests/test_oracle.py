@@ -151,6 +151,13 @@ def test_model_points_golden(oracle):
 
 
 def test_qp_kkt(oracle):
+    """KKT of the oracle's QP solutions (HPIPM-style stop: mu, bound, stationarity and equality
+    residuals, cap 50).  Stationarity is checked on every QP that met the stop test, against
+    1e-8 relative plus the dual-accuracy floor every primal-dual IPM has here: an active bound's
+    multiplier comes from lam/t * (v - lo - t), whose difference carries eps*|v| of rounding, so
+    lam is known to ~ (lam/t) eps |v| ~ eps |v| lam^2 / mu, and the adjoint sums that over the
+    horizon (it grows as mu_stop shrinks, ~1e-3 absolute at mu = 1e-10 on
+    the QPs with lam ~ 100 active s bounds; most QPs sit far below it)."""
     from qp_data import build_qp
     N, nb = 20, 32
     op = make_opts(N=N, sqp_iters=3)
@@ -162,25 +169,33 @@ def test_qp_kkt(oracle):
     A, B, b, H, g, lo, hi, act, dx0 = build_qp(oracle, op, r["X"], r["U"], yref, yref_e, x0)
     s = oracle.qp(op, A, B, b, H, g, lo, hi, act, dx0)
     assert s["fail"] == 0
-    conv = s["iters"] < op.qp_iters            # QPs that met mu < mu_stop within the cap
-    assert conv.mean() > 0.9
+    conv = s["qp_status"] == 0                  # stop test met (2: iteration cap)
+    assert conv.all()
+    eps = np.finfo(float).eps
+    plain = []
     for i in np.where(conv)[0]:
         dx, du, pi, lam = s["dx"][i], s["du"][i], s["pi"][i], s["lam"][i]
         np.testing.assert_allclose(dx[0], dx0[i], atol=1e-15)
+        v = np.stack([dx[:N, 3], du[:, 0], du[:, 1]], 1)
+        t = np.stack([v - lo[i], hi[i] - v], 2).reshape(N, 6)
+        sig = np.where(np.repeat(act[i], 2, 1) > 0, np.abs(lam) / np.maximum(np.abs(t), 1e-300), 0.0)
+        floor = N * sig.max() * eps * max(np.abs(lo[i]).max(), np.abs(hi[i]).max())
+        scale = 1 + np.abs(g[i]).max()
+        worst = 0.0
         for k in range(N):
             # dynamics
             np.testing.assert_allclose(dx[k + 1], A[i, k] @ dx[k] + B[i, k] @ du[k] + b[i, k], atol=1e-12)
             # bounds (IPM: interior up to the final barrier parameter)
-            v = np.array([dx[k, 3], du[k, 0], du[k, 1]])
-            sl = slice(0 if k >= 1 else 1, 3)
-            assert np.all(v[sl] >= lo[i, k, sl] - 1e-8) and np.all(v[sl] <= hi[i, k, sl] + 1e-8)
+            sl = slice(0 if (k >= 1 or act[i, 0, 0]) else 1, 3)
+            assert np.all(v[k, sl] >= lo[i, k, sl] - 1e-8) and np.all(v[k, sl] <= hi[i, k, sl] + 1e-8)
             # stationarity w.r.t. u_k
             rs = H[i, 6 * k + 4:6 * k + 6] * du[k] + g[i, 6 * k + 4:6 * k + 6] + B[i, k].T @ pi[k] \
                 - lam[k, 2::2] + lam[k, 3::2]
-            scale = 1 + np.abs(B[i, k].T @ pi[k]).max()
-            # IPM accuracy at mu_stop = 1e-10: the u_t directions carry only tau*W_u = 5e-5 of
-            # curvature, so barrier-level residuals (mu/t) stay visible
-            assert np.abs(rs).max() < 1e-3 * scale, (i, k, rs)
+            worst = max(worst, np.abs(rs).max())
+        assert worst <= 1e-8 * scale + floor, (i, worst, floor)
+        plain.append(worst <= 1e-8 * scale)
+    # the floor binds only on the QPs with strongly active bounds
+    assert np.mean(plain) >= 0.75, np.mean(plain)
 
 
 def test_config1_closed_loop_golden(oracle):

@@ -29,6 +29,8 @@ class Options(C.Structure):
         ("tol_stat", C.c_double), ("tol_eq", C.c_double), ("tol_ineq", C.c_double), ("tol_comp", C.c_double),
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
         ("res_stop", C.c_double),
+        ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
+        ("stage0_s_bound", C.c_int32), ("pad2_", C.c_int32),
     ]
 
 
@@ -77,6 +79,7 @@ _SIGS = {
     "qsp_get_status": [_P, _P],
     "qsp_get_sqp_iter": [_P, _P],
     "qsp_get_qp_iter": [_P, _P],
+    "qsp_get_qp_capped": [_P, _P],
     "qsp_get_time_tot": [_P, C.POINTER(_D)],
     "qsp_set_reference_trajectory": [_P, _P, _I],
     "qsp_set_reference_trajectories": [_P, _P, _I],
@@ -95,7 +98,7 @@ _SIGS = {
     "qsp_eval_dynamics": [_P, _I, _P, _P, _P, _P, _P],
     "qsp_eval_rk4": [_P, _I, _P, _D, _P, _P, _P, _P, _P],
     "qsp_eval_vbound": [_P, _I, _P, _P, _P],
-    "qsp_qp_solve": [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "qsp_qp_solve": [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "qsp_last_error": [],
 }
 _VOID = {"qsp_default_options"}

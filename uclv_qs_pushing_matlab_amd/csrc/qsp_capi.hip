@@ -54,7 +54,7 @@ struct qsp_solver {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int n_shapes = 0;
-    DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, cost;
+    DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, qp_capped, cost;
     DevBuf warm_valid, traj, index_time;
     DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit, whist;
     DevBuf scratch[12];
@@ -72,15 +72,19 @@ struct qsp_solver {
     SqpStreams split;
     int parts_req = 0;
     int fused_req = -1;            // QSP_FUSED_LOOP (-1: auto)
+    int cus = 256;                 // compute units of the device (hipDeviceProp multiProcessorCount)
 };
 
 // --------------------------------------------------------------- helpers
 static const SqpStreams* sqp_split(qsp_solver* s) {
-    s->split.parts = s->parts_req > 0 ? s->parts_req : sqp_parts_auto(s->o.batch, s->o.N, s->S);
+    s->split.parts = s->parts_req > 0 ? s->parts_req : sqp_parts_auto(s->o.batch, s->o.N, s->S, s->cus);
     // the whole SQP loop in one launch: auto for batches below one fill of the wave slots
-    // when one part is in use; QSP_FUSED_LOOP=0/1 overrides (experiments, parity tests)
-    s->split.fused = s->fused_req >= 0 ? s->fused_req
-                                       : (s->split.parts == 1 && sqp_fused_auto(s->o.batch, s->o.N, s->S, s->o.nlp_mode));
+    // when one part is in use; QSP_FUSED_LOOP=0/1 overrides (experiments, parity tests) where
+    // the fused kernel exists (nlp_mode 0, S = 1 or 2)
+    const bool can_fuse = s->o.nlp_mode == QSP_NLP_SQP_RTI_FIXED && (s->S == 1 || s->S == 2);
+    s->split.fused = !can_fuse ? 0
+                   : s->fused_req >= 0 ? s->fused_req
+                   : (s->split.parts == 1 && sqp_fused_auto(s->o.batch, s->o.N, s->S, s->o.nlp_mode, s->cus));
     if (s->split.fused) s->split.parts = 1;
     return &s->split;
 }
@@ -110,6 +114,10 @@ static void fill_params(qsp_solver* s) {
     p.sigma_min = s->o.sigma_min;
     p.mu_stop = s->o.mu_stop;
     p.res_stop = s->o.res_stop;
+    p.qp_tol_stat = s->o.qp_tol_stat;
+    p.qp_tol_eq = s->o.qp_tol_eq;
+    p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
+    p.pad_ = 0;
     p.tol_stat = s->o.tol_stat;
     p.tol_eq = s->o.tol_eq;
     p.tol_ineq = s->o.tol_ineq;
@@ -187,6 +195,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.status = s->status.as<int32_t>();
     a.sqp_iter = s->sqp_iter.as<int32_t>();
     a.qp_iter = s->qp_iter.as<int32_t>();
+    a.qp_capped = s->qp_capped.as<int32_t>();
     a.cost = s->cost.as<double>();
     a.wX = s->wX.as<double>();
     a.wU = s->wU.as<double>();
@@ -278,7 +287,7 @@ void qsp_default_options(qsp_options* o) {
     o->batch = 1;
     o->nlp_mode = QSP_NLP_SQP_RTI_FIXED;
     o->sqp_iters = 50;
-    o->qp_iters = 20;
+    o->qp_iters = 50;               // acados qp_solver_iter_max default
     o->stages_per_lane = 0;
     o->device = 0;
     o->cost_scale_Ts = 1;
@@ -289,6 +298,9 @@ void qsp_default_options(qsp_options* o) {
     o->sigma_min = 1e-2;
     o->mu_stop = 1e-10;
     o->res_stop = 1e-10;
+    o->qp_tol_stat = 1e-10;
+    o->qp_tol_eq = 1e-10;
+    o->stage0_s_bound = 1;          // acados: bgh constraints on stages 0..N-1
     // nlp_mode 1: NMPC_controller.m:275-276 tolerances; acados merit_backtracking defaults
     o->tol_stat = o->tol_eq = o->tol_ineq = o->tol_comp = 1e-6;
     o->ls_alpha_min = 0.05;
@@ -311,6 +323,9 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
         return fail(QSP_ERR_ARG, "qsp_create: nlp_mode 1 needs N+1 <= 64 (one stage per lane), "
                                  "0 < ls_alpha_red < 1 and 0 < ls_alpha_min <= 1");
     if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
+    if (o->qp_iters > 255) return fail(QSP_ERR_ARG, "qsp_create: qp_iters must be <= 255");
+    if (!(o->qp_tol_stat > 0.0) || !(o->qp_tol_eq > 0.0) || !(o->mu_stop > 0.0) || !(o->res_stop > 0.0))
+        return fail(QSP_ERR_ARG, "qsp_create: QP stop tolerances must be > 0");
     if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");
     int S = o->stages_per_lane > 0 ? o->stages_per_lane : (o->nlp_mode == QSP_NLP_SQP_MERIT ? 1 : auto_S(o->N));
     if (S < 1 || S > 2) return fail(QSP_ERR_ARG, "qsp_create: stages_per_lane must be 1 or 2");
@@ -320,6 +335,11 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     qsp_solver* s = new qsp_solver();
     s->o = *o;
     s->S = S;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, o->device) == hipSuccess && prop.multiProcessorCount > 0)
+            s->cus = prop.multiProcessorCount;
+    }
     fill_params(s);
     // reference defaults (main.m:82-90, NMPC_controller.m:16-26, 98-100, 251-252)
     const double W[6] = {1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3};
@@ -354,6 +374,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->status, B * 4);
     al(s->sqp_iter, B * 4);
     al(s->qp_iter, B * 4);
+    al(s->qp_capped, B * 4);
     al(s->cost, B * 8);
     al(s->warm_valid, B);
     al(s->wX, B * (N + 1) * 4 * 8);
@@ -402,7 +423,8 @@ int qsp_destroy(qsp_solver* s) {
     if (!s) return QSP_OK;
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
-                      &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->cost, &s->warm_valid,
+                      &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->qp_capped, &s->cost,
+                      &s->warm_valid,
                       &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
                       &s->whist};
     for (DevBuf* b : bufs) b->release();
@@ -618,6 +640,10 @@ int qsp_get_qp_iter(qsp_solver* s, int32_t* it) {
     if (!s || !it) return fail(QSP_ERR_ARG, "qsp_get_qp_iter: null argument");
     return d2h(s, it, s->qp_iter, (size_t)s->o.batch * 4);
 }
+int qsp_get_qp_capped(qsp_solver* s, int32_t* c) {
+    if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_qp_capped: null argument");
+    return d2h(s, c, s->qp_capped, (size_t)s->o.batch * 4);
+}
 int qsp_get_time_tot(qsp_solver* s, double* ms) {
     if (!s || !ms) return fail(QSP_ERR_ARG, "qsp_get_time_tot: null argument");
     *ms = (double)s->last_ms;
@@ -731,7 +757,8 @@ int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int3
     for (int32_t t = 0; t < n_steps; ++t) {
         HIPCHK(launch_controller_step(s, t));                                  // y_ref for index0 + t
         HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s), sqp_split(s)));   // NMPC_controller.solve
-        HIPCHK(launch_plant(s->shapes.as<ShapeDev>(), s->shape_id.as<int32_t>(), (int)B, s->o.Ts, s->x0.as<double>(),
+        HIPCHK(launch_plant(s->shapes.as<ShapeDev>(), s->n_shapes, s->shape_id.as<int32_t>(), (int)B, s->o.Ts,
+                            s->x0.as<double>(),
                             s->u0.as<double>(), s->status.as<int32_t>(), t, n_steps,
                             (nz && t + 1 < n_steps) ? nz + (size_t)(t + 1) * B * 4 : nullptr, dX.as<double>(),
                             dU.as<double>(), dS.as<int32_t>(), s->stream));
@@ -914,7 +941,7 @@ int qsp_eval_vbound(qsp_solver* s, int32_t n, const int32_t* sid, const double* 
 
 int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, const double* b, const double* H,
                  const double* g, const double* lo, const double* hi, const double* dx0, double* dx, double* du,
-                 double* pi, double* lam, int32_t* iters) {
+                 double* pi, double* lam, int32_t* iters, int32_t* qp_status) {
     if (!s || nb < 1 || !A || !B || !b || !H || !g || !lo || !hi || !dx0 || !dx || !du || !pi || !lam || !iters)
         return fail(QSP_ERR_ARG, "qsp_qp_solve: bad argument");
     const int N = s->o.N;
@@ -975,6 +1002,7 @@ int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, co
     HIPCHK(sc[4].ensure((size_t)nb * (N + 1) * 32)); HIPCHK(sc[5].ensure((size_t)nb * N * 16));
     HIPCHK(sc[6].ensure((size_t)nb * N * 32)); HIPCHK(sc[7].ensure((size_t)nb * N * 48));
     HIPCHK(sc[8].ensure((size_t)nb * 4));
+    HIPCHK(sc[9].ensure((size_t)nb * 4));
     SolveArgs a;
     std::memset(&a, 0, sizeof a);
     a.p = p;
@@ -982,12 +1010,26 @@ int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, co
     a.wlin = sc[0].as<double>(); a.wX = sc[1].as<double>(); a.wU = sc[2].as<double>(); a.wx0 = sc[3].as<double>();
     a.qp_dx = sc[4].as<double>(); a.qp_du = sc[5].as<double>(); a.PI_out = sc[6].as<double>();
     a.qp_lam = sc[7].as<double>(); a.qp_iter = sc[8].as<int32_t>();
+    a.qp_capped = sc[9].as<int32_t>();
     HIPCHK(launch_qp(a, s->S, s->stream));
     if ((r = stage_out(s, dx, sc[4], (size_t)nb * (N + 1) * 4)) || (r = stage_out(s, du, sc[5], (size_t)nb * N * 2)) ||
         (r = stage_out(s, pi, sc[6], (size_t)nb * N * 4)) || (r = stage_out(s, lam, sc[7], (size_t)nb * N * 6)) ||
         (r = stage_out(s, iters, sc[8], (size_t)nb)))
         return r;
+    std::vector<int32_t> qst(qp_status ? (size_t)nb : 0);
+    if (qp_status && (r = stage_out(s, qst.data(), sc[9], (size_t)nb))) return r;
     HIPCHK(hipStreamSynchronize(s->stream));
+    if (qp_status) {
+        for (int l = 0; l < nb; ++l) {
+            bool fin = true;
+            for (int q = 0; q < (N + 1) * 4; ++q) fin = fin && std::isfinite(dx[(size_t)l * (N + 1) * 4 + q]);
+            for (int q = 0; q < N * 2; ++q) fin = fin && std::isfinite(du[(size_t)l * N * 2 + q]);
+            // the stage-0 s is fixed (dx_0 = dx0): outside its bounds the QP is infeasible
+            const bool infeas = s->p.s0_bound && (dx0[(size_t)l * 4 + 3] < lo[(size_t)l * N * 3] ||
+                                                  dx0[(size_t)l * 4 + 3] > hi[(size_t)l * N * 3]);
+            qp_status[l] = !fin ? 1 : (infeas ? 3 : qst[l]);
+        }
+    }
     return QSP_OK;
 }
 

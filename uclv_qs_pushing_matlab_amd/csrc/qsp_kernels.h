@@ -36,6 +36,7 @@ struct SolveArgs {
     int32_t* status;           // B
     int32_t* sqp_iter;         // B
     int32_t* qp_iter;          // B (sum of IPM iterations)
+    int32_t* qp_capped;        // B (QPs stopped by the iteration cap; nullptr: not counted)
     double* cost;              // B
     // workspace (device, owned by the handle)
     double* wX;                // B x (N+1) x 4   SQP iterate
@@ -79,14 +80,16 @@ struct SqpStreams {
 // timed as a whole (qsp_get_kernel_times then reports K qp_step "launches" = SQP iterations).
 hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t* ev = nullptr,
                       const SqpStreams* split = nullptr);
-int sqp_parts_auto(int B, int N, int S);
-int sqp_fused_auto(int B, int N, int S, int nlp_mode);
+// cus: compute units of the handle's device (hipDeviceProp multiProcessorCount; 256 on a whole
+// MI355X, fewer on a partitioned one)
+int sqp_parts_auto(int B, int N, int S, int cus);
+int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
 hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
                                    hipStream_t stream);
-hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
-                        const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
-                        double* Utraj, int32_t* Straj, hipStream_t stream);
+hipError_t launch_plant(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
+                        const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
+                        double* Xtraj, double* Utraj, int32_t* Straj, hipStream_t stream);
 hipError_t launch_straight_lines(int B, int T, const double* x0, const double* xf, double t0, double tf, double Ts,
                                  int auto_angle, double* traj, hipStream_t stream);
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,

@@ -33,6 +33,7 @@
 
 #include <atomic>
 
+#include "../../include/qsp_nmpc.h"
 #include "qsp_math.hpp"
 #include "qsp_kernels.h"
 
@@ -139,7 +140,10 @@ __device__ __forceinline__ int sidx(int i, int j) {
 // better: over 50 SQP iterations of the bench workload (oracle counts, 3 instances per
 // wave) waves run 1.066x the mean iteration count instead of 1.095x with the last count
 // alone (1.239x unsorted).
-constexpr int PACK_KEYS_MAX = 1024;   // (qp_iters + 1)^2 keys; packing needs qp_iters <= 31
+constexpr int PACK_KEYS_MAX = 1024;   // (maxkey + 1)^2 keys
+// key levels: IPM counts above 31 share the last level (qp_iters up to 50 and more: the
+// acados default cap; such QPs are rare, ~0.1 % of the bench workload's)
+__host__ __device__ __forceinline__ int pack_maxkey(int qp_iters) { return qp_iters < 31 ? qp_iters : 31; }
 __device__ __forceinline__ int pack_key(int packed, int maxkey) {
     const int last = min(max(packed & 0xff, 0), maxkey), prev = min(max((packed >> 8) & 0xff, 0), maxkey);
     return (maxkey - last) * (maxkey + 1) + (maxkey - prev);
@@ -193,6 +197,13 @@ struct Ctx {
 
 template <int S>
 __device__ __forceinline__ int kof(const Ctx& c, int ls) { return c.lig * S + ls; }
+
+// Is bound side j (0 = s, 1 = u_n, 2 = u_t) of stage k part of the QP?  Stages 0..N-1; the s
+// bound at stage 0 only with stage0_s_bound (s_0 is fixed by x0 there: the pair is a
+// constant slack that enters the complementarity measure, NMPC_controller.m:237,251-252).
+__device__ __forceinline__ bool bnd_act(const Ctx& c, const SolveParams& p, int k, int j) {
+    return (k < c.N) && (j > 0 || k >= 1 || p.s0_bound != 0);
+}
 
 // bounds of the QP step of slot ls: lo = lh - v, hi = uh - v, v = (s, u_n, u_t)
 template <int S>
@@ -371,7 +382,7 @@ __device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const bool act = bnd_act(c, p, k, j);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double sl = ll * st.rt(ls, 2 * j), sh = lh * st.rt(ls, 2 * j + 1);
         const double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
@@ -395,7 +406,7 @@ __device__ __forceinline__ void affine_dirs(const Ctx& c, const SolveParams& p, 
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const bool act = bnd_act(c, p, k, j);
         const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double sl = ll * st.rt(ls, 2 * j), sh = lh * st.rt(ls, 2 * j + 1);
@@ -415,13 +426,14 @@ __device__ __forceinline__ void affine_dirs(const Ctx& c, const SolveParams& p, 
 
 // Complementarity after the affine step aa (Mehrotra's mu_aff), from the cached directions.
 template <int S>
-__device__ __forceinline__ double affine_mu_part(const Ctx& c, const Stage<S>& st, int ls, const double at[6],
+__device__ __forceinline__ double affine_mu_part(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
+                                                 const double at[6],
                                                  const double al[6], double aa) {
     const int k = kof<S>(c, ls);
     double part = 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const bool act = bnd_act(c, p, k, j);
         const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double dtl = act ? at[2 * j] : 0.0, dth = act ? at[2 * j + 1] : 0.0;
@@ -434,12 +446,13 @@ __device__ __forceinline__ double affine_mu_part(const Ctx& c, const Stage<S>& s
 // Corrector barrier gradient change of slot ls from the cached affine directions (the
 // Hessian is the predictor's): hg[3+j] = c_h / t_h - c_l / t_l, c = sigma mu - dt_aff dl_aff.
 template <int S>
-__device__ __forceinline__ void corrector_terms(const Ctx& c, const Stage<S>& st, int ls, const double at[6],
+__device__ __forceinline__ void corrector_terms(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
+                                                const double at[6],
                                                 const double al[6], double smu) {
     const int k = kof<S>(c, ls);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const bool act = bnd_act(c, p, k, j);
         const double cl = smu - at[2 * j] * al[2 * j], ch = smu - at[2 * j + 1] * al[2 * j + 1];
         st.hg(ls, 3 + j) = act ? ch * st.rt(ls, 2 * j + 1) - cl * st.rt(ls, 2 * j) : 0.0;
     }
@@ -456,7 +469,7 @@ __device__ __forceinline__ void corrector_dirs(const Ctx& c, const SolveParams& 
     bnd_lohi<S>(p, st, ls, lo, hi);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const bool act = (k < c.N) && (j > 0 || k >= 1);
+        const bool act = bnd_act(c, p, k, j);
         const double tl = st.t(ls, 2 * j), th = st.t(ls, 2 * j + 1);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double rtl = st.rt(ls, 2 * j), rth = st.rt(ls, 2 * j + 1);
@@ -667,21 +680,31 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 
 // Mehrotra predictor-corrector IPM on the current linearisation.  Leaves the
 // damped control step in LDS (F_DU) and the slacks/multipliers in F_T / F_LM.
-// Returns the number of iterations taken by this lane's instance.
+// Returns the number of iterations taken by this lane's instance; `conv` tells whether the
+// stop test was met (false: the iteration cap stopped it, as HPIPM at iter_max).
+//
+// Stop test (HPIPM's four exit residuals, ocp_qp_ipm): complementarity mu < mu_stop, bound
+// residual < res_stop, stationarity < qp_tol_stat, equality < qp_tol_eq.  The three linear
+// residuals are those of the IPM iterate (z, pi, lam, t) with start z = 0, pi = 0, lam =
+// mu0 / t: every Newton step solves them exactly and the update scales all of them by
+// (1 - alpha), so each is its start value times prod(1 - alpha) (tracked, not recomputed:
+// r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)).
 template <int S>
-__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool skip = false) {
-    const double m = 2.0 * (3.0 * c.N - 1.0);
+__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool& conv,
+                      bool skip = false) {
+    const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
     // initial point.  r0 = largest bound residual of the infeasible start (t - d where the
     // slack had to be floored at t_min); every update scales all residuals by (1 - alpha)
-    double r0 = 0.0;
+    double r0 = 0.0, rg0 = 0.0, rb0 = 0.0;
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         const int k = kof<S>(c, ls);
         double lo[3], hi[3];
         bnd_lohi<S>(p, st, ls, lo, hi);
+        double gl[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const bool act = (k < c.N) && (j > 0 || k >= 1);
+            const bool act = bnd_act(c, p, k, j);
             const double tl = fmax(-lo[j], p.t_min), th = fmax(hi[j], p.t_min);
             if (act) r0 = fmax(r0, fmax(tl + lo[j], th - hi[j]));
             const double rl = rcp(tl), rh = rcp(th);
@@ -691,6 +714,15 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
             st.rt(ls, 2 * j + 1) = act ? rh : 1.0;
             st.lm(ls, 2 * j) = act ? p.mu0 * rl : 0.0;
             st.lm(ls, 2 * j + 1) = act ? p.mu0 * rh : 0.0;
+            gl[j] = act ? p.mu0 * rh - p.mu0 * rl : 0.0;
+        }
+        // start-point stationarity g + C' lam (bounded components s, u_n, u_t) and equality
+        // (defects; x0 on the first stage); the padding slots past the terminal stage hold zeros
+        if (k <= c.N) {
+            rg0 = fmax(rg0, fmax(fmax(fabs(st.g[ls][0]), fabs(st.g[ls][1])), fmax(fabs(st.g[ls][2]), fabs(st.g[ls][3] + gl[0]))));
+            rg0 = fmax(rg0, fmax(fabs(st.g[ls][4] + gl[1]), fabs(st.g[ls][5] + gl[2])));
+            rb0 = fmax(rb0, fmax(fmax(fabs(st.bb[ls][0]), fabs(st.bb[ls][1])), fmax(fabs(st.bb[ls][2]), fabs(st.bb[ls][3]))));
+            if (k == 0) rb0 = fmax(rb0, fmax(fmax(fabs(dx0[0]), fabs(dx0[1])), fmax(fabs(dx0[2]), fabs(dx0[3]))));
         }
         st.du(ls, 0) = 0.0;
         st.du(ls, 1) = 0.0;
@@ -703,18 +735,22 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         }
     }
     r0 = group_max(r0, c.gs);
+    rg0 = group_max(rg0, c.gs);
+    rb0 = group_max(rb0, c.gs);
     double rscale = 1.0;
     int nit = 0;
-    for (int it = 0; it < p.qp_iters; ++it) {
+    for (int it = 0;; ++it) {
         double tl_sum = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls)
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.gs) / m;
-        // stop on complementarity AND bound feasibility (as HPIPM checks both)
-        const bool done = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop));
-        if (__ballot(!done) == 0ull) break;
+        const bool done = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop) &&
+                                   !(rg0 * rscale >= p.qp_tol_stat) && !(rb0 * rscale >= p.qp_tol_eq));
+        conv = done;
+        // the cap is tested after the last step too (conv reports it), then the loop ends
+        if (it == p.qp_iters || __ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
         // ---- predictor
 #pragma unroll
@@ -729,14 +765,14 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         const double aa = group_min(num / den, c.gs);
         double ma = 0.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) ma += affine_mu_part<S>(c, st, ls, at[ls], al[ls], aa);
+        for (int ls = 0; ls < S; ++ls) ma += affine_mu_part<S>(c, p, st, ls, at[ls], al[ls], aa);
         const double mua = group_sum(ma, c.gs) / m;
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
         const double smu = sg * mu;
         // ---- corrector
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, st, ls, at[ls], al[ls], smu);
+        for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, p, st, ls, at[ls], al[ls], smu);
         riccati_solve<S, false>(c, p, st, dx0, F_VN, M);
         double dt[S][6], dl[S][6];
         num = 1.0; den = p.frac;       // initial bound 1/frac
@@ -852,6 +888,18 @@ __device__ __forceinline__ void nlp_init(const SolveArgs& A, int i, bool use_pi)
     A.wdone[i] = 0;
 }
 
+// With the stage-0 s bound in the QP (stage0_s_bound), s_0 = x0's s is a fixed quantity of
+// every QP: outside [lh_s, uh_s] every QP of the solve is infeasible.  The instance then does
+// not iterate (wdone = 3: status QSP_STATUS_QP_FAIL, sqp_iter 0, the initial guess returned),
+// as the oracle's sqp_solve.  (Called after nlp_init, which clears wdone.)
+__device__ __forceinline__ void s0_feasible(const SolveArgs& A, int i, double s0) {
+    const SolveParams& p = A.p;
+    if (p.s0_bound && A.wdone && !(s0 >= p.lh[0] && s0 <= p.uh[0])) {
+        A.wdone[i] = 3;
+        A.sqp_iter[i] = 0;
+    }
+}
+
 // NMPC_controller.solve prologue (NMPC_controller.m:332-384) or acados-level init copy.
 __global__ void prologue_kernel(SolveArgs A) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -864,6 +912,7 @@ __global__ void prologue_kernel(SolveArgs A) {
     double* X = A.wX + (size_t)i * (N + 1) * 4;
     double* U = A.wU + (size_t)i * N * 2;
     A.qp_iter[i] = 0;
+    if (A.qp_capped) A.qp_capped[i] = 0;
     if (A.wdone) A.wdone[i] = 0;
     if (A.wnit) A.wnit[i] = 0;
     if (!(A.flags & QSP_FLAG_CONTROLLER)) {
@@ -871,6 +920,7 @@ __global__ void prologue_kernel(SolveArgs A) {
         for (int q = 0; q < N * 2; ++q) U[q] = A.U_in[(size_t)i * N * 2 + q];
         for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
         if (p.nlp_mode == 1) nlp_init(A, i, true);
+        s0_feasible(A, i, x0[3]);
         return;
     }
     x0[3] = mat_mod(x0[3], sh.b) - sh.b * ((x0[3] < 0.0) ? 1.0 : 0.0);   // :332
@@ -896,6 +946,7 @@ __global__ void prologue_kernel(SolveArgs A) {
         dynamics<false>(sh, xc[2], xc[3], U[2 * k], U[2 * k + 1], d);
         for (int c = 0; c < 4; ++c) xc[c] = xc[c] + p.Ts * d.f[c];
     }
+    s0_feasible(A, i, x0[3]);
 }
 
 // The QP of one SQP iteration in the register/LDS-resident lane-group layout:
@@ -956,7 +1007,7 @@ __device__ __forceinline__ double merit_stage(const SolveParams& p, int k, const
     const double v[3] = {x[3], u[0], u[1]};
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        if (j == 0 && k == 0) continue;
+        if (j == 0 && k == 0 && !p.s0_bound) continue;
         const double vl = p.lh[j] - v[j], vh = v[j] - p.uh[j];
         if (vl > 0.0) ph += eta[2 * j] * vl;
         if (vh > 0.0) ph += eta[2 * j + 1] * vh;
@@ -1012,7 +1063,7 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
         const double v[3] = {st.v(0, 0), st.v(0, 1), st.v(0, 2)};
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            if (j == 0 && k == 0) continue;
+            if (j == 0 && k == 0 && !p.s0_bound) continue;
             const double sl = v[j] - p.lh[j], sh_ = p.uh[j] - v[j];
             ri = fmax(ri, fmax(-sl, -sh_));
             rc = fmax(rc, fmax(fabs(LAMk[2 * j] * sl), fabs(LAMk[2 * j + 1] * sh_)));
@@ -1138,8 +1189,11 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             A.sqp_iter[iv] = it;
         }
     }
-    const int nit = qp_ipm<S>(c, p, st, dx0, skip);
+    bool conv;
+    const int nit = qp_ipm<S>(c, p, st, dx0, conv, skip);
     qp_rollout<S>(c, st, dx0);
+    // QPs stopped by the iteration cap (their last iterate is used, as HPIPM's at iter_max)
+    if (A.qp_capped && c.real && c.lig == 0 && !skip && !conv) A.qp_capped[iv] += 1;
     // a non-finite QP solution stops the instance's SQP with its last iterate (status 1),
     // as the oracle's sqp_solve does
     bool failed = false;
@@ -1164,7 +1218,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         const int old = A.wnit[iv];
         const int rec = (MERIT || !(skip || failed)) ? pack_record(old, nit) : old;
         A.wnit[iv] = rec;
-        if (A.whist) atomicAdd(&A.whist[(it & 1) * PACK_KEYS_MAX + pack_key(rec, p.qp_iters)], 1);
+        if (A.whist) atomicAdd(&A.whist[(it & 1) * PACK_KEYS_MAX + pack_key(rec, pack_maxkey(p.qp_iters))], 1);
     }
     if constexpr (MERIT) {
         // QP solution (step, dynamics and bound multipliers) for the line-search kernel
@@ -1200,6 +1254,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
                 for (int q = 0; q < 6; ++q) A.qp_lam[((size_t)iv * N + k) * 6 + q] = st.lm(ls, q);
             }
             if (k == 0) A.qp_iter[iv] = nit;
+            if (k == 0 && A.qp_capped) A.qp_capped[iv] = conv ? 0 : 2;   // QP status: 0 stop test met, 2 cap
         }
         return;
     }
@@ -1238,6 +1293,11 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
     bool stopped = false;   // group-uniform: a failed QP stops the instance's SQP
     for (int it = 0; it < p.sqp_iters; ++it) {
         if (it > 0) __syncthreads();   // the neighbour lanes' X, U stores of the last iteration
+        // debug: re-poisoned at every SQP iteration, so a read of a word the current iteration
+        // did not write shows up (the last iteration's finite values would hide it)
+        if (it > 0 && (A.flags & QSP_FLAG_POISON)) {
+            for (int f = 0; f < F_COUNT * S; ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
+        }
         // lane geometry and addresses re-derived every iteration from an opaque lane id: hoisted
         // out of the loop they would stay live through the interior point (register budget)
         int lane = threadIdx.x & 63;
@@ -1305,8 +1365,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
 #pragma unroll
         for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
         const bool skip = stopped || !c.real;
-        const int nit = qp_ipm<S>(c, p, st, dx0, skip);
+        bool conv;
+        const int nit = qp_ipm<S>(c, p, st, dx0, conv, skip);
         qp_rollout<S>(c, st, dx0);
+        if (A.qp_capped && c.real && c.lig == 0 && !skip && !conv) A.qp_capped[iv] += 1;
         double bad = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) {
@@ -1485,7 +1547,7 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
         const double v[3] = {xk[3], uk[0], uk[1]};
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            if (j == 0 && k == 0) continue;
+            if (j == 0 && k == 0 && !p.s0_bound) continue;
             const double lo = p.lh[j] - v[j], hi = p.uh[j] - v[j];
             if (lo > 0.0) dph -= ETAk[2 * j] * lo;
             if (hi < 0.0) dph -= ETAk[2 * j + 1] * (-hi);
@@ -1569,8 +1631,10 @@ __global__ void epilogue_kernel(SolveArgs A) {
     for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s += p.We[q] * r * r; bad |= !isfinite(X[4 * N + q]); }
     cost += 0.5 * s;
     A.cost[i] = cost;
-    const int fr = A.wdone ? A.wdone[i] : 0;                   // 1 converged, 2 failed QP (sqp_iter written then)
-    if (p.nlp_mode == 1) A.status[i] = (bad || fr == 2) ? 1 : (fr == 1 ? 0 : 2);
+    // wdone: 1 converged, 2 failed QP, 3 infeasible stage-0 bound (sqp_iter written then)
+    const int fr = A.wdone ? A.wdone[i] : 0;
+    if (fr == 3) A.status[i] = QSP_STATUS_QP_FAIL;
+    else if (p.nlp_mode == 1) A.status[i] = (bad || fr == 2) ? 1 : (fr == 1 ? 0 : 2);
     else A.status[i] = (bad || fr == 2) ? 1 : 0;
     if (fr == 0) A.sqp_iter[i] = p.sqp_iters;
     A.u0[(size_t)i * 2] = U[0];
@@ -1612,12 +1676,13 @@ __global__ void closed_loop_init_kernel(int B, double* x, const double* noise0, 
     }
 }
 
-__global__ void plant_kernel(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
-                             const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
-                             double* Utraj, int32_t* Straj) {
+__global__ void plant_kernel(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
+                             const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
+                             double* Xtraj, double* Utraj, int32_t* Straj) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
-    const ShapeDev& sh = shapes[sid ? sid[i] : 0];
+    const int id = sid ? sid[i] : 0;   // clamped like shape_of (the table may have shrunk since the ids were set)
+    const ShapeDev& sh = shapes[id < 0 ? 0 : (id >= n_shapes ? n_shapes - 1 : id)];
     double xi[4] = {x[(size_t)i * 4], x[(size_t)i * 4 + 1], x[(size_t)i * 4 + 2], x[(size_t)i * 4 + 3]};
     const double u[2] = {u0[(size_t)i * 2], u0[(size_t)i * 2 + 1]};
     DynOut d;
@@ -1640,11 +1705,11 @@ hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, doubl
     return hipGetLastError();
 }
 
-hipError_t launch_plant(const ShapeDev* shapes, const int32_t* sid, int B, double Ts, double* x, const double* u0,
-                        const int32_t* status, int step, int n_steps, const double* noise_next, double* Xtraj,
-                        double* Utraj, int32_t* Straj, hipStream_t stream) {
-    hipLaunchKernelGGL(plant_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, shapes, sid, B, Ts, x, u0, status,
-                       step, n_steps, noise_next, Xtraj, Utraj, Straj);
+hipError_t launch_plant(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
+                        const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
+                        double* Xtraj, double* Utraj, int32_t* Straj, hipStream_t stream) {
+    hipLaunchKernelGGL(plant_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, shapes, n_shapes, sid, B, Ts, x, u0,
+                       status, step, n_steps, noise_next, Xtraj, Utraj, Straj);
     return hipGetLastError();
 }
 
@@ -1787,14 +1852,14 @@ static hipError_t launch_sqp_loop(const SolveArgs& a, hipStream_t stream) {
 }
 
 // sqp_loop_kernel keeps more state live across its SQP loop than qp_step_kernel and runs at
-// 1 wave/SIMD (256 VGPRs + AGPRs), so it pays only while its waves fit the 1 024 SIMDs in one
-// round.  Measured (scripts/fused_sweep.sh, N = 20, K = 50, S = 1, solves/s per-iteration
-// launches -> fused): B = 1 024 58.7k -> 76.5k; 2 048 115k -> 123k; 3 072 (1 024 waves) 173k ->
-// 224k; 4 096 (1 366 waves, two rounds) 227k -> 169k.
-int sqp_fused_auto(int B, int N, int S, int nlp_mode) {
+// 1 wave/SIMD (256 VGPRs + AGPRs), so it pays only while its waves fit the SIMDs (4 per CU:
+// 1 024 on a whole MI355X) in one round.  Measured (scripts/fused_sweep.sh, N = 20, K = 50,
+// S = 1, solves/s per-iteration launches -> fused): B = 1 024 58.7k -> 76.5k; 2 048 115k ->
+// 123k; 3 072 (1 024 waves) 173k -> 224k; 4 096 (1 366 waves, two rounds) 227k -> 169k.
+int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus) {
     const int G = 64 / lanes_per_instance(N, S);
     const long waves = ((long)B + G - 1) / G;
-    return (nlp_mode == 0 && waves <= 1024) ? 1 : 0;
+    return (nlp_mode == 0 && (S == 1 || S == 2) && waves <= 4L * cus) ? 1 : 0;
 }
 
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
@@ -1822,16 +1887,16 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     return hipGetLastError();
 }
 
-// Two parts once the batch fills the 2 048 wave slots of the chip (2 waves/SIMD) at least once;
+// Two parts once the batch fills the wave slots of the device (2 waves/SIMD) at least once;
 // below that the waves of one launch already run side by side and splitting only adds launches.
 // Measured (scripts/parts_sweep.sh, N = 20, K = 50, solves/s one part -> two parts): B = 4 096
 // (1 366 waves) 226k -> 218k; B = 8 192 323k -> 361k; B = 16 384 423k -> 505k; B = 32 768
 // 473k -> 509k; B = 65 536 491k -> 512k; N = 50, B = 16 384 (S = 2) 69.7k -> 74.8k; merit
 // SQP (max_iter 30) B = 65 536 619k -> 672k, and at N = 10 1.42M -> 1.65M.
-int sqp_parts_auto(int B, int N, int S) {
+int sqp_parts_auto(int B, int N, int S, int cus) {
     const int G = 64 / lanes_per_instance(N, S);
     const long waves = ((long)B + G - 1) / G;
-    return waves >= 2048 ? 2 : 1;
+    return waves >= 8L * cus ? 2 : 1;   // 2 waves/SIMD x 4 SIMDs per CU: 2 048 slots on a whole MI355X
 }
 
 // One part's SQP loop on `stream`: (packing sort, QP [+ line search]) x sqp_iters over the
@@ -1841,7 +1906,7 @@ static hipError_t sqp_iteration(const SolveArgs& as, int S, bool sorted, int it,
     hipError_t e = hipSuccess;
     if (sorted && it > 0) {
         hipLaunchKernelGGL(sort_by_iters_kernel, dim3((as.nI + 255) / 256), dim3(256), 0, stream, as.i0, as.nI,
-                           as.p.qp_iters, as.wnit, as.wperm, as.whist, (it - 1) & 1);
+                           pack_maxkey(as.p.qp_iters), as.wnit, as.wperm, as.whist, (it - 1) & 1);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = mark();
@@ -1872,12 +1937,14 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(prologue_kernel, dim3(gb), dim3(128), 0, stream, a);
     e = hipGetLastError();
-    const bool sorted = !fused && a.wperm && a.wnit && a.whist &&
-                        (a.p.qp_iters + 1) * (a.p.qp_iters + 1) <= PACK_KEYS_MAX;
+    const bool sorted = !fused && a.wperm && a.wnit && a.whist;
     SolveArgs as = a;
     as.i0 = 0;
     as.nI = a.B;
-    if (!sorted) as.whist = nullptr;
+    if (!sorted) {   // identity order: the QP kernels must not read an unsorted permutation
+        as.whist = nullptr;
+        as.wperm = nullptr;
+    }
     if (e == hipSuccess && sorted) {
         hipLaunchKernelGGL(iota_kernel, dim3(gb), dim3(128), 0, stream, a.B, a.wperm);
         e = hipGetLastError();

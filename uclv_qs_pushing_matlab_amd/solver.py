@@ -21,8 +21,9 @@ class OcpSolver:
     # metric), 'SQP' = merit backtracking + KKT tolerances (the reference's own options)
     NLP_MODES = {"SQP_RTI": 0, "SQP": 1}
 
-    def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
+    def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=50, stages_per_lane=0, device=0,
                  cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10,
+                 qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=True,
                  nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
                  timings=False):
         L = _lib.lib()
@@ -33,6 +34,8 @@ class OcpSolver:
         o.cost_scale_Ts = 1 if cost_scale_Ts else 0
         o.mu0, o.t_min, o.frac, o.sigma_min, o.mu_stop = mu0, t_min, frac, sigma_min, mu_stop
         o.res_stop = res_stop
+        o.qp_tol_stat, o.qp_tol_eq = float(qp_tol_stat), float(qp_tol_eq)
+        o.stage0_s_bound = 1 if stage0_s_bound else 0
         if nlp_solver_type not in self.NLP_MODES:
             raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
         o.nlp_mode = self.NLP_MODES[nlp_solver_type]
@@ -190,10 +193,10 @@ class OcpSolver:
             fn = {"x": self._L.qsp_get_x, "u": self._L.qsp_get_u, "pi": self._L.qsp_get_pi}[field]
             check(fn(self._h, ptr(out)), f"get('{field}')")
             return out if stage is None else out[:, stage]
-        if field in ("status", "sqp_iter", "qp_iter"):
+        if field in ("status", "sqp_iter", "qp_iter", "qp_capped"):
             out = np.zeros(B, np.int32)
             fn = {"status": self._L.qsp_get_status, "sqp_iter": self._L.qsp_get_sqp_iter,
-                  "qp_iter": self._L.qsp_get_qp_iter}[field]
+                  "qp_iter": self._L.qsp_get_qp_iter, "qp_capped": self._L.qsp_get_qp_capped}[field]
             check(fn(self._h, ptr(out)), f"get('{field}')")
             return out
         if field == "time_tot":
@@ -348,6 +351,7 @@ class OcpSolver:
         dx, du = np.zeros((nb, N + 1, 4)), np.zeros((nb, N, 2))
         pi, lam = np.zeros((nb, N, 4)), np.zeros((nb, N, 6))
         iters = np.zeros(nb, np.int32)
+        qst = np.zeros(nb, np.int32)
         check(self._L.qsp_qp_solve(self._h, nb, *[ptr(a) for a in arrs], ptr(dx), ptr(du), ptr(pi), ptr(lam),
-                                   ptr(iters)), "qsp_qp_solve")
-        return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters)
+                                   ptr(iters), ptr(qst)), "qsp_qp_solve")
+        return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters, qp_status=qst)
