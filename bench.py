@@ -1,18 +1,17 @@
 #!/usr/bin/env python3
 """Benchmark: batched pusher-slider NMPC solves/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the configuration the metric is quoted on):
-  N = 20, batch = 65 536 lanes per GPU, 4 slider shapes mixed per lane
-  (shape_id = lane mod 4: santal/balea/montana/pulirapid), K = 50 SQP-RTI
-  (full Gauss-Newton) iterations, every lane a cold-start NMPC_controller.solve
-  (acados_nmpc/NMPC_controller.m:329-423), x0 drawn from the config-2 law
-  (ranges of main.m:53-56), x_ref = the config-1 straight line from index 1.
-A step is one batched solve of all lanes; inputs are resident in HBM before the
-timed region, which brackets exactly --steps kernel launches.
-
-Multi-GPU (torchrun): one process per GPU, each rank solves its own shard of
-65 536 lanes (weak scaling, no data-path collective); the timing is the max over
-ranks.  Rank 0 prints one JSON line.
+Workload at N = 1 GPU (BASELINE configs[2], the configuration the metric is quoted on):
+  N = 20, batch = 65 536 lanes, 4 slider shapes mixed per lane (shape_id = lane mod 4:
+  santal/balea/montana/pulirapid), K = 50 SQP-RTI (full Gauss-Newton) iterations, every lane a
+  cold-start NMPC_controller.solve (acados_nmpc/NMPC_controller.m:329-423), x0 drawn from the
+  config-2 law (ranges of main.m:53-56), x_ref = the config-1 straight line from index 1.
+Workload at N > 1 GPUs (BASELINE configs[3]): the same law over a global batch of 262 144 lanes
+  split into contiguous shards, one process per GPU (strong scaling: 131 072 lanes per GPU at
+  N = 2, 32 768 at N = 8), no collective on the data path; after the timed region the u0/status
+  of all shards are all-gathered over RCCL (xGMI), timed separately ("gather_ms").
+A step is one batched solve of all lanes; inputs are resident in HBM before the timed region,
+which brackets exactly --steps solves.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -61,11 +60,39 @@ def make_inputs(B, N, seed, lo=0, hi=None):
     return x0, yref, yref_e, shape_id, traj
 
 
-def shard_range(total, world, rank):
-    """Contiguous, balanced shard of `total` units for `rank` (covers every unit once)."""
-    base, rem = divmod(total, world)
-    lo = rank * base + min(rank, rem)
-    return lo, lo + base + (1 if rank < rem else 0)
+from uclv_qs_pushing_matlab_amd.sharding import gather_lanes, shard_range  # noqa: E402,F401  (re-exported)
+
+CONFIG2_BATCH = 65536          # BASELINE configs[2]: one GPU
+CONFIG3_BATCH = 262144         # BASELINE configs[3]: sharded over the GPUs of one node
+SEED = 20250303 + 3
+
+
+def config1_inputs(N, B=4096, seed=20250303 + 1):
+    """BASELINE configs[1]: B = 4 096 random x0 (config-2 law) around santal, straight x_ref."""
+    x0 = config2_x0(B, seed)
+    traj = straight_traj()
+    return x0, traj, np.zeros(B, np.int32)
+
+
+def host_cpu():
+    """Host CPU facts for the cpu_baseline record: nproc, the CPUs this process may run on,
+    the model name, and the worker threads used (OMP_NUM_THREADS when set: the GPU box sets it
+    to this job's CPU share; otherwise every CPU of the affinity mask)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return dict(nproc=os.cpu_count(), affinity_cpus=aff, model=model, threads=max(1, env or aff))
 
 
 def flops_per_solve(N, K, qp_iter_total):
@@ -96,24 +123,62 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0):
     return n, dt, r, run
 
 
+def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp):
+    """GPU u0 vs oracle u0 on the whole CPU sample (n lanes), with the oracle's own sensitivity
+    as the yardstick: a lane is chaotic when the oracle's u0 moves by > 1e-9 under
+    three 1e-13 relative perturbations of x0 or when mu_stop moves 1e-10 -> 1.5e-10; parity is
+    asserted (informatively here, in tests/test_gpu_config2.py as a test) on the others."""
+    u0_ref = r["u0"]
+    d = np.abs(u0_gpu[:n] - u0_ref).max(1)
+    self_dev = np.zeros(n)
+    for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+        self_dev = np.maximum(self_dev, np.abs(run(slice(0, n), x0[:n] * (1 + sgn * f * 1e-13))["u0"] - u0_ref).max(1))
+    mu_dev = np.abs(run(slice(0, n), mu_stop=1.5e-10)["u0"] - u0_ref).max(1)
+    nonchaotic = (self_dev < 1e-9) & (mu_dev < 1e-9)
+    out = {"lanes": int(n), "max_abs_u0_err": float(d.max()),
+           "nonchaotic_lanes": int(nonchaotic.sum()),
+           "max_abs_u0_err_nonchaotic": float(d[nonchaotic].max()) if nonchaotic.any() else None,
+           "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
+           "oracle_self_frac_le_1e-6": float(np.mean(self_dev <= 1e-6)),
+           "chaotic_frac": float(np.mean(self_dev > 1e-6)),
+           "qp_rule": "HPIPM-style: mu, bound, stationarity, equality residuals < 1e-10, cap 20, stall exit, stage-0 s bound"}
+    if nlp == "SQP_RTI":
+        # the same statistics with round 1's QP stop rule (mu and bound residual < 1e-10, cap 20,
+        # no stage-0 s bound), on the first lanes: the chaotic fraction does not depend on it
+        m = min(n, 2048)
+        r01 = dict(qp_iters=20, qp_tol_stat=float("inf"), qp_tol_eq=float("inf"), stage0_s_bound=0, qp_stall_iters=0)
+        base = run(slice(0, m), **r01)["u0"]
+        dev = np.zeros(m)
+        for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+            dev = np.maximum(dev, np.abs(run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13), **r01)["u0"] - base).max(1))
+        out["chaotic_frac_first"] = {"lanes": int(m), "this_rule": float(np.mean(self_dev[:m] > 1e-6)),
+                                     "round1_rule": float(np.mean(dev > 1e-6))}
+    out["note"] = ("u0_ref = CPU oracle (acados parity unpinned); nonchaotic = the oracle itself moves < 1e-9 under "
+                   "three 1e-13 relative x0 perturbations and mu_stop 1.5e-10")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="lanes per GPU")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="lanes over all GPUs (0: 65 536 = configs[2] on one GPU, 262 144 = configs[3] on several)")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--sqp-iters", type=int, default=50)
-    ap.add_argument("--qp-iters", type=int, default=50)
+    ap.add_argument("--qp-iters", type=int, default=20)
     ap.add_argument("--stages-per-lane", type=int, default=0)
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
                     help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] (B = 4 096) side measurement")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
                     help="SQP_RTI: fixed-K full steps (the BASELINE metric); SQP: the reference's merit-backtracking "
                          "SQP with KKT tolerances (sqp_iters = max_iter)")
-    ap.add_argument("--seed", type=int, default=20250303 + 3)
+    ap.add_argument("--seed", type=int, default=SEED)
+    ap.add_argument("--dump-u0", default=None, help="rank 0 writes the gathered u0/status (.npz) here")
     args = ap.parse_args()
 
     import torch
@@ -131,16 +196,16 @@ def main():
         torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
     dev = torch.device("cuda", gpu)
-    red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the timing reductions
+    red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the reductions and the gather
 
     from uclv_qs_pushing_matlab_amd._lib import DeviceIO
     from uclv_qs_pushing_matlab_amd.objects import make_shape
     from uclv_qs_pushing_matlab_amd.solver import OcpSolver
 
-    B, N, K = args.batch, args.N, args.sqp_iters
-    # this rank's shard of the global lane set (weak scaling: B lanes per GPU)
-    lo, hi = shard_range(B * world, world, rank)
-    x0, yref, yref_e, sid, traj = make_inputs(B * world, N, args.seed, lo, hi)
+    N, K = args.N, args.sqp_iters
+    total = args.global_batch or (CONFIG2_BATCH if world == 1 else CONFIG3_BATCH)
+    lo, hi = shard_range(total, world, rank)        # this rank's shard of the global lane set
+    x0, yref, yref_e, sid, traj = make_inputs(total, N, args.seed, lo, hi)
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
@@ -200,9 +265,32 @@ def main():
     # per-lane IPM iteration counts of the (identical) timed solves -> algorithmic flops
     solver.synchronize()
     qp_iter = solver.get("qp_iter")
-    status = d_st.cpu().numpy()
-    u0 = d_u0.cpu().numpy()
-    flops_solve = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())   # all lanes, one solve
+    qp_capped = solver.get("qp_capped")
+
+    # the trivial gather (north_star): u0 and status of every shard to every rank, one fixed-size
+    # all_gather each over RCCL (device tensors; gloo: host tensors), timed on its own
+    gather_ms = None
+    if dist:
+        g_u0, g_st = d_u0.to(red_dev), d_st.to(red_dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        u0_all = gather_lanes(g_u0, total, dist, world, rank)
+        st_all = gather_lanes(g_st, total, dist, world, rank)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        tt = torch.tensor([gather_ms], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        gather_ms = float(tt.item())
+        u0_all, status_all = u0_all.cpu().numpy(), st_all.cpu().numpy()
+    else:
+        u0_all, status_all = d_u0.cpu().numpy(), d_st.cpu().numpy()
+    u0 = u0_all[lo:hi]
+    nbad = int(np.count_nonzero(status_all))
+    if rank == 0 and args.dump_u0:
+        np.savez(args.dump_u0, u0=u0_all, status=status_all)
+
+    flops_solve = float(flops_per_solve(N, K, qp_iter.astype(np.float64)).sum())   # this shard, one solve
     # dominant kernel: qp_step (one launch = one SQP iteration's QP for every lane of the shard).
     # With two stream parts the two half launches of an SQP iteration overlap each other and
     # the next iteration's, so the library times the whole loop (fork -> join on the launch
@@ -214,34 +302,36 @@ def main():
     qp_flops_launch = float(qp_iter.astype(np.float64).sum()) * N * FLOP_IPM_STAGE / K
     if args.nlp == "SQP_RTI":   # the SQP iteration's linearisation runs inside the qp_step launch
         qp_flops_launch += float(Bl) * N * FLOP_LIN_STAGE
-    if dist:
-        tt = torch.tensor([float(np.count_nonzero(status))], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        nbad = int(tt[0])
-    else:
-        nbad = int(np.count_nonzero(status))
 
-    total_solves = B * world * args.steps
+    total_solves = total * args.steps
     value = total_solves / elapsed
     avg_kern_s = float(np.mean(kern_ms)) * 1e-3
     achieved = qp_flops_launch / qp_avg_s / 1e12
+    if world == 1:
+        workload = f"BASELINE configs[2]: batch={total} on 1 GPU"
+    else:
+        workload = (f"BASELINE configs[3]: global batch={total} sharded over {world} GPUs "
+                    f"({Bl} lanes on rank {rank}), u0/status all-gathered over "
+                    f"{'RCCL' if backend == 'nccl' else backend} after the timed region")
 
     result = {
         "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"BASELINE configs[2]: batch={B} per GPU, N={N}, 4 shapes mixed per lane, "
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": workload + f", N={N}, 4 shapes mixed per lane, "
                                + (f"K={K} SQP-RTI iterations" if args.nlp == "SQP_RTI" else
                                   f"merit-backtracking SQP, max_iter={K}, tol 1e-6")
                                + ", cold-start NMPC_controller.solve per lane",
-                   "global_batch": B * world, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
+                   "global_batch": total, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
                    "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
                               "stream_parts": parts},
-                   "parallelism": f"dp{world} (independent lane shards, no collective in the solve)"},
+                   "parallelism": f"dp{world} (contiguous lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
+        "qp_capped_frac": float(qp_capped.sum() / (Bl * K)),
         "status_nonzero_lanes": nbad,
+        "gather_ms": gather_ms,
         "kernels_ms_avg": {k: (v[0] / v[1] if v[1] else None) for k, v in ktimes.items()},
         "roofline": {"bound": "mfma", "kernel": "qp_step_kernel",
                      "peak_kind": "FP64 vector (= FP64 matrix) dense peak; the kernel is FP64-VALU bound",
@@ -262,9 +352,9 @@ def main():
         except Exception:
             pass
 
-    # host-boundary rate (not `value`): NMPC_controller.solve through the C ABI with x0 in
-    # host memory and u0 copied back, y_ref staged on the device from the shared table
     if world == 1:
+        # host-boundary rate (not `value`): NMPC_controller.solve through the C ABI with x0 in
+        # host memory and u0 copied back, y_ref staged on the device from the shared table
         solver.set_shape_ids(sid)
         solver.set_reference_trajectory(traj)
         solver.controller_solve(x0, 1)
@@ -275,53 +365,54 @@ def main():
             solver.controller_reset()
             solver.controller_solve(x0, 1)
         result["host_boundary_solves_per_s"] = Bl * nrep / (time.perf_counter() - th)
+    solver.close()
+
+    if rank == 0 and world == 1 and not args.no_configs1:
+        # BASELINE configs[1] beside the headline (its own GPU timing; CPU in full below)
+        x1, traj1, sid1 = config1_inputs(N)
+        s1 = OcpSolver(N=N, batch=len(x1), sqp_iters=K, qp_iters=args.qp_iters, device=gpu, nlp_solver_type=args.nlp)
+        s1.set_shapes([make_shape("santal")], shape_id=sid1)
+        s1.set_reference_trajectory(traj1)
+        s1.controller_solve(x1, 1)
+        s1.synchronize()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(10):
+            s1.controller_reset()
+            s1.controller_solve(x1, 1)
+        result["configs1"] = {"workload": "BASELINE configs[1]: batch=4096 santal, N=20, K=50 SQP-RTI, cold start",
+                              "gpu_solves_per_s": len(x1) * 10 / (time.perf_counter() - t1),
+                              "note": "host-boundary controller solves (x0 in, u0 out), 10 repeats"}
+        u1_gpu = s1.get_u0()
+        s1.close()
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        threads = max(1, min(threads, 16))
+        hc = host_cpu()
+        threads = hc["threads"]
         n, dt, r, run = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, 1 if args.nlp == "SQP" else 0)
         result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-                                  "sample": f"{n} lanes of the same workload (oracle/qsp_oracle.c, OpenMP, "
-                                            f"{dt:.1f} s)"}
-        # parity on the sampled lanes: GPU u0 vs oracle u0 (same cold-start controller solve)
-        u0_ref = r["u0"]
-        d = np.abs(u0[:n] - u0_ref).max(1)
-        m = min(n, 512)
-        # a lane is 'stable' when the oracle itself stays put (< 1e-9) under three 1e-13 relative
-        # perturbations of x0: the full-step SQP amplifies rounding on the other lanes
-        stable = np.ones(m, bool)
-        self_dev = np.zeros(m)   # how far the oracle itself moves under the perturbations
-        for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
-            rp = run(slice(0, m), x0[:m] * (1 + sgn * f * 1e-13))
-            dev = np.abs(rp["u0"] - u0_ref[:m]).max(1)
-            stable &= dev < 1e-9
-            self_dev = np.maximum(self_dev, dev)
-        # ... and converged (the K-1 and K iterates agree: not a limit cycle of the full-step SQP)
-        if args.nlp == "SQP_RTI":
-            stable &= np.abs(run(slice(0, m), K_run=K - 1)["u0"] - u0_ref[:m]).max(1) < 1e-9
-            # ... and insensitive to where the IPM stop test (mu < mu_stop) fires
-            stable &= np.abs(run(slice(0, m), mu_stop=1.5e-10)["u0"] - u0_ref[:m]).max(1) < 1e-9
-        else:   # merit SQP: the lanes that met the KKT tolerances
-            stable &= r["status"][:m] == 0
-        result["parity"] = {"max_abs_u0_err": float(d.max()), "lanes": int(n),
-                            "max_abs_u0_err_stable_lanes": float(d[:m][stable].max()) if stable.any() else None,
-                            "stable_lanes": int(stable.sum()), "stable_checked": int(m),
-                            "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
-                            # the same statistic for the oracle against itself under 1e-13 relative
-                            # perturbations of x0 (first `stable_checked` lanes): the GPU/oracle gap
-                            # on the remaining lanes is the problem's own sensitivity
-                            "frac_lanes_err_le_1e-6_first": float(np.mean(d[:m] <= 1e-6)),
-                            "oracle_self_frac_le_1e-6_first": float(np.mean(self_dev <= 1e-6)),
-                            "note": "u0_ref = CPU oracle (acados parity unpinned); 'stable' = oracle itself moves "
-                                    "< 1e-9 under three 1e-13 relative perturbations of x0, between K-1 and K "
-                                    "iterations and with mu_stop 1.5e-10 (converged, non-chaotic lane)"}
+                                  "host_nproc": hc["nproc"], "host_affinity_cpus": hc["affinity_cpus"],
+                                  "cpu_model": hc["model"],
+                                  "sample": f"{n} lanes of the same workload (oracle/qsp_oracle.c, OpenMP over "
+                                            f"{threads} threads, {dt:.1f} s)"}
+        result["parity"] = parity_leg(u0, x0, traj, sid, N, K, n, r, run, args.nlp)
+        if "configs1" in result:
+            x1, traj1, sid1 = config1_inputs(N)
+            from oracle.oracle import Oracle, make_opts
+            orc = Oracle(SHAPES)
+            tc = time.perf_counter()
+            r1 = orc.controller_solve(make_opts(N=N, sqp_iters=K, nlp_mode=1 if args.nlp == "SQP" else 0), x1, traj1,
+                                      1, orc.new_warm(len(x1), N), shape_id=sid1, nthreads=threads)
+            dtc = time.perf_counter() - tc
+            result["configs1"].update({"cpu_solves_per_s": len(x1) / dtc, "cpu_seconds": dtc, "cpu_threads": threads,
+                                       "cpu_kind": "port (the full batch)",
+                                       "frac_lanes_err_le_1e-6": float(np.mean(np.abs(u1_gpu - r1["u0"]).max(1) <= 1e-6))})
     if rank == 0:
         if nbad:
-            print(f"bench: WARNING {nbad} of {B * world} lanes returned a non-zero status", file=sys.stderr)
+            print(f"bench: WARNING {nbad} of {total} lanes returned a non-zero status", file=sys.stderr)
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
-    solver.close()
 
 
 if __name__ == "__main__":

@@ -73,11 +73,16 @@ typedef struct {
     double res_stop;          /* interior point stops when mu < mu_stop AND the bound residual < res_stop */
     /* ... AND (HPIPM's other two exit residuals, ocp_qp_ipm res_g / res_b) the stationarity and
      * equality residuals of the IPM iterate are below these (tracked exactly: each Newton step
-     * scales them by 1 - alpha); qp_iters (default 50, acados qp_solver_iter_max) caps it */
+     * scales them by 1 - alpha); qp_iters caps it (default 20: acados' qp_solver_iter_max 50 is
+     * selectable; measured no change in the SQP's rounding sensitivity, 2.3x slower at B = 4 096) */
     double qp_tol_stat, qp_tol_eq;
     int32_t stage0_s_bound;   /* 1 (default): the s bound of h also applies at stage 0 (acados bgh on
                                  stages 0..N-1, NMPC_controller.m:237,251-252); 0: stages 1..N-1 */
-    int32_t pad2_;
+    int32_t qp_stall_iters;   /* stall exit (generalises HPIPM's alpha_min exit): a QP whose step length
+                                 stays below qp_stall_alpha for qp_stall_iters consecutive iterations is
+                                 locally infeasible (mu grows without bound) and stops there, counted as
+                                 capped; default 3 x 1e-3, 0 = off (runs to qp_iters as HPIPM would) */
+    double qp_stall_alpha;
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */

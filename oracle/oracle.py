@@ -43,18 +43,20 @@ class Opts(C.Structure):
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
         ("res_stop", C.c_double),
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
+        ("qp_stall_alpha", C.c_double), ("qp_stall_iters", C.c_int32), ("pad2_", C.c_int32),
     ]
 
 
-def make_opts(N=20, sqp_iters=50, qp_iters=50, Ts=0.05, tau=None,
+def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
               W=(1.0, 1.0, 1e-3, 0.0, 1e-3, 1e-3), We=(2e5, 2e5, 20.0, 0.0),
               lh=(-0.06, 0.0, -0.05), uh=(0.011, 0.03, 0.05),
               mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
               u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
-              qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1):
+              qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1, qp_stall_alpha=1e-3, qp_stall_iters=3):
     o = Opts()
     o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, int(stage0_s_bound)
     o.qp_tol_stat, o.qp_tol_eq = qp_tol_stat, qp_tol_eq
+    o.qp_stall_alpha, o.qp_stall_iters = qp_stall_alpha, int(qp_stall_iters)
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W

@@ -86,6 +86,12 @@ typedef struct {
      * them by (1 - alpha): tracked as r_0 * prod(1 - alpha) from the start point (z = 0, pi = 0,
      * lam = mu0 / t), like the bound residual. */
     double qp_tol_stat, qp_tol_eq;
+    /* stall exit: a QP whose step length stays below qp_stall_alpha for qp_stall_iters
+     * consecutive iterations is locally infeasible (e.g. the linearised s dynamics cannot meet
+     * the s bound): mu grows without bound and alpha ~1e-5 to the cap.  It stops there, with
+     * the capped QPs' status (its last iterate is used, as at the cap).  0 iterations: off. */
+    double qp_stall_alpha;
+    int32_t qp_stall_iters, pad2_;
 } or_opts;
 
 /* ================================================================ dual numbers */
@@ -474,7 +480,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         if (fabs(qp->dx0[i]) > rb0) rb0 = fabs(qp->dx0[i]);
     }
 
-    int nit = 0, converged = 0;
+    int nit = 0, converged = 0, stall = 0;
     for (int it = 0; it <= o->qp_iters && !infeasible; ++it) {
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
@@ -483,6 +489,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         if (!(mu >= o->mu_stop) && !(r0 * rscale >= o->res_stop) && !(rg0 * rscale >= o->qp_tol_stat) &&
             !(rb0 * rscale >= o->qp_tol_eq)) { converged = 1; break; }
         if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
+        if (o->qp_stall_iters > 0 && stall >= o->qp_stall_iters) break;   /* stalled: as at the cap */
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
@@ -539,6 +546,7 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         }
         double alpha = o->frac * amax;
         if (alpha > 1.0) alpha = 1.0;
+        stall = alpha < o->qp_stall_alpha ? stall + 1 : 0;
         rscale *= 1.0 - alpha;
         for (int q = 0; q < 6 * N; ++q) { t[q] += alpha * dta[q]; lam[q] += alpha * dla[q]; }
         for (int k = 0; k < N; ++k)

@@ -10,8 +10,8 @@ run() {
   timeout -k 10 300 python bench.py --no-cpu --steps 5 --warmup 1 "$@" > gpurun_out/configs/$name.json 2> gpurun_out/configs/$name.err || exit $?
   python -c "import json;d=json.load(open('gpurun_out/configs/$name.json'));print('$name', round(d['value']), 'solves/s', round(d['ms_per_step'],2), 'ms/solve', 'frac', round(d['roofline']['frac'],4))"
 }
-run cfg1_B4096 --batch 4096
-run cfg2_B65536 --batch 65536
-run cfg3_B32768 --batch 32768
-run cfg4_N50_B16384 --N 50 --batch 16384
-run mainm_N10_SQP --N 10 --batch 65536 --nlp SQP --sqp-iters 30
+run cfg1_B4096 --global-batch 4096
+run cfg2_B65536 --global-batch 65536
+run cfg3_B32768 --global-batch 32768
+run cfg4_N50_B16384 --N 50 --global-batch 16384
+run mainm_N10_SQP --N 10 --global-batch 65536 --nlp SQP --sqp-iters 30

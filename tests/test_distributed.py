@@ -1,10 +1,13 @@
-"""CPU, world_size 2 over gloo: the multi-GPU layout of bench.py (independent lane
-shards, max-over-ranks timing, optional gather of u0) reproduces the single-process
-result.  The per-shard solve here is the CPU oracle (no GPU in this container)."""
+"""CPU, world_size 2 (and 3) over gloo: the multi-GPU layout of bench.py -- its input law per
+shard (bench.make_inputs), its shard split and its u0/status gather
+(uclv_qs_pushing_matlab_amd.sharding.shard_range / gather_lanes), the max-over-ranks timing --
+reproduces the single-process result.  The per-shard solve here is the CPU oracle (no GPU in
+this container); tests/test_gpu_multirank.py runs the same path on the HIP library."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -23,18 +26,20 @@ def _worker(rank, world, port, total, out):
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bench import make_inputs
     from oracle.oracle import Oracle, make_opts
+    from uclv_qs_pushing_matlab_amd.sharding import gather_lanes
     lo, hi = shard_range(total, world, rank)
-    x0 = config2_x0(total, 123)[lo:hi]
+    x0, _, _, sid, traj = make_inputs(total, 10, 123, lo, hi)
     orc = Oracle()
-    r = orc.controller_solve(make_opts(N=10, sqp_iters=2), x0, straight_traj(), 1, orc.new_warm(hi - lo, 10),
-                             shape_id=np.arange(lo, hi) % 4, nthreads=1)
+    r = orc.controller_solve(make_opts(N=10, sqp_iters=2), x0, traj, 1, orc.new_warm(hi - lo, 10),
+                             shape_id=sid, nthreads=1)
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    parts = [None] * world
-    dist.all_gather_object(parts, (lo, r["u0"]))
+    u0 = gather_lanes(torch.as_tensor(r["u0"]), total, dist, world, rank)
+    st = gather_lanes(torch.as_tensor(r["status"]), total, dist, world, rank)
     if rank == 0:
-        out.put((float(t), parts))
+        out.put((float(t), u0.numpy(), st.numpy()))
     dist.destroy_process_group()
 
 
@@ -48,26 +53,27 @@ def test_shard_range_covers_all_lanes():
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_two_rank_gloo_matches_single_process():
+@pytest.mark.parametrize("world,total", [(2, 24), (3, 25)])
+def test_multi_rank_gloo_matches_single_process(world, total):
+    from bench import make_inputs
     from oracle.oracle import Oracle, make_opts
-    total, world = 24, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
     for p in procs:
         p.start()
-    tmax, parts = q.get(timeout=300)
+    tmax, u0, st = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert tmax == 2.0                                   # max over ranks
-    u0 = np.concatenate([u for _, u in sorted(parts, key=lambda t: t[0])])
+    assert tmax == float(world)                          # max over ranks
     orc = Oracle()
-    x0 = config2_x0(total, 123)
-    ref = orc.controller_solve(make_opts(N=10, sqp_iters=2), x0, straight_traj(), 1, orc.new_warm(total, 10),
-                               shape_id=np.arange(total) % 4, nthreads=1)
-    np.testing.assert_array_equal(u0, ref["u0"])
+    x0, _, _, sid, traj = make_inputs(total, 10, 123)
+    ref = orc.controller_solve(make_opts(N=10, sqp_iters=2), x0, traj, 1, orc.new_warm(total, 10),
+                               shape_id=sid, nthreads=1)
+    np.testing.assert_array_equal(u0, ref["u0"])           # shards unequal at total = 25: padded gather
+    np.testing.assert_array_equal(st, ref["status"])
 
 
 def test_make_inputs_shards_match_single_process():

@@ -30,7 +30,7 @@ class Options(C.Structure):
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
         ("res_stop", C.c_double),
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
-        ("stage0_s_bound", C.c_int32), ("pad2_", C.c_int32),
+        ("stage0_s_bound", C.c_int32), ("qp_stall_iters", C.c_int32), ("qp_stall_alpha", C.c_double),
     ]
 
 

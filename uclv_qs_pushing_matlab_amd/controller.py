@@ -19,7 +19,7 @@ from .solver import OcpSolver
 
 
 class NMPCController:
-    def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=50,
+    def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=20,
                  device=0, stages_per_lane=0):
         # create_ocp_opts (:270-300): 'SQP' with merit backtracking, max_iter 30, tol 1e-6;
         # nlp_solver_type='SQP_RTI' gives the fixed-K full-step iteration of the BASELINE metric

@@ -117,7 +117,8 @@ static void fill_params(qsp_solver* s) {
     p.qp_tol_stat = s->o.qp_tol_stat;
     p.qp_tol_eq = s->o.qp_tol_eq;
     p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
-    p.pad_ = 0;
+    p.qp_stall_iters = s->o.qp_stall_iters;
+    p.qp_stall_alpha = s->o.qp_stall_alpha;
     p.tol_stat = s->o.tol_stat;
     p.tol_eq = s->o.tol_eq;
     p.tol_ineq = s->o.tol_ineq;
@@ -287,7 +288,7 @@ void qsp_default_options(qsp_options* o) {
     o->batch = 1;
     o->nlp_mode = QSP_NLP_SQP_RTI_FIXED;
     o->sqp_iters = 50;
-    o->qp_iters = 50;               // acados qp_solver_iter_max default
+    o->qp_iters = 20;               // acados qp_solver_iter_max is 50: measured no effect on chaos, 2.3x slower at B = 4 096
     o->stages_per_lane = 0;
     o->device = 0;
     o->cost_scale_Ts = 1;
@@ -301,6 +302,8 @@ void qsp_default_options(qsp_options* o) {
     o->qp_tol_stat = 1e-10;
     o->qp_tol_eq = 1e-10;
     o->stage0_s_bound = 1;          // acados: bgh constraints on stages 0..N-1
+    o->qp_stall_iters = 3;          // stall exit: alpha < 1e-3 three times in a row
+    o->qp_stall_alpha = 1e-3;
     // nlp_mode 1: NMPC_controller.m:275-276 tolerances; acados merit_backtracking defaults
     o->tol_stat = o->tol_eq = o->tol_ineq = o->tol_comp = 1e-6;
     o->ls_alpha_min = 0.05;
@@ -324,6 +327,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
                                  "0 < ls_alpha_red < 1 and 0 < ls_alpha_min <= 1");
     if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
     if (o->qp_iters > 255) return fail(QSP_ERR_ARG, "qsp_create: qp_iters must be <= 255");
+    if (o->qp_stall_iters < 0) return fail(QSP_ERR_ARG, "qsp_create: qp_stall_iters must be >= 0");
     if (!(o->qp_tol_stat > 0.0) || !(o->qp_tol_eq > 0.0) || !(o->mu_stop > 0.0) || !(o->res_stop > 0.0))
         return fail(QSP_ERR_ARG, "qsp_create: QP stop tolerances must be > 0");
     if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");

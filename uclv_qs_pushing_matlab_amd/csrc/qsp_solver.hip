@@ -738,7 +738,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
     rg0 = group_max(rg0, c.gs);
     rb0 = group_max(rb0, c.gs);
     double rscale = 1.0;
-    int nit = 0;
+    int nit = 0, stall = 0;
     for (int it = 0;; ++it) {
         double tl_sum = 0.0;
 #pragma unroll
@@ -746,9 +746,11 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.gs) / m;
-        const bool done = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop) &&
-                                   !(rg0 * rscale >= p.qp_tol_stat) && !(rb0 * rscale >= p.qp_tol_eq));
-        conv = done;
+        conv = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop) && !(rg0 * rscale >= p.qp_tol_stat) &&
+                        !(rb0 * rscale >= p.qp_tol_eq));
+        // stall exit (locally infeasible QP: the step length stays tiny while mu grows): stops
+        // like the cap, after the stop test had its chance
+        const bool done = conv || (p.qp_stall_iters > 0 && stall >= p.qp_stall_iters);
         // the cap is tested after the last step too (conv reports it), then the loop ends
         if (it == p.qp_iters || __ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
@@ -780,6 +782,8 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int ls = 0; ls < S; ++ls) corrector_dirs<S>(c, p, st, ls, at[ls], al[ls], smu, dt[ls], dl[ls], num, den);
         double alpha = p.frac * group_min(num / den, c.gs);
         alpha = fmin(alpha, 1.0);
+        // (a finished instance keeps its count: it sits the rest of the wave's loop out at alpha = 0)
+        stall = done ? stall : (alpha < p.qp_stall_alpha ? stall + 1 : 0);
         if (done) alpha = 0.0;
         rscale *= 1.0 - alpha;
 #pragma unroll
