@@ -94,6 +94,8 @@ typedef struct {
     double b;                           /* contour length (bspline_shape.m:37)           */
     double c_ellipse;                   /* tau_max / (mu_sg m g)  (PusherSliderModel.m:55) */
     double mu_sp;                       /* pusher-slider friction                        */
+    double xwidth;                      /* slider width along x (object_selection.m; the
+                                           disturbance re-projection, helper.m:229)       */
 } qsp_shape;
 
 /* Device-resident I/O for qsp_solve_device (all pointers on the handle's device). */
@@ -185,6 +187,36 @@ int qsp_controller_reset(qsp_solver* s);                                        
  * status_traj: B x n_steps (found_sol = status == 0) or NULL. */
 int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int32_t n_steps, const double* noise,
                     double* X_traj, double* U_traj, int32_t* status_traj);
+/* closed_loop_matlab's other branches (helper.m:195-322) */
+typedef struct {
+    double plant_delay;        /* plant.time_delay [s]: the plant applies u delayed by ceil(delay/Ts) steps
+                                  (u_buff_plant, helper.m:211-212, 289-296) */
+    int32_t disturbance;       /* disturbance_: at step t_dist (1-based) y += amplitude and the contact
+                                  point is re-projected onto the contour (helper.m:221-236) */
+    int32_t t_dist;
+    const double* amplitude;   /* B amplitude_dist per lane (NULL: 0) */
+} qsp_closed_loop_opts;
+/* Per step i: disturbance (i == t_dist), noise, the controller's delay prediction (delay_buffer_sim
+ * with the handle's delay compensation), u = solve(x_sim, index0 + i - 1 + delay_buff_comp), the
+ * controller buffer push, the (delayed) plant step.  X_traj: the plant states after disturbance and
+ * noise (B x (n+1) x 4); X_sim (optional): the states handed to the solver (B x n x 4). */
+int qsp_closed_loop_ex(qsp_solver* s, const qsp_closed_loop_opts* opts, const double* x0, const int32_t* index0,
+                       int32_t n_steps, const double* noise, double* X_traj, double* X_sim, double* U_traj,
+                       int32_t* status_traj);
+/* set_delay_comp (NMPC_controller.m:106-110): delay_buff_comp = ceil(delay / Ts) columns; the
+ * reference table is read as set_reference_trajectory prepends it (:425-431) and the per-lane input
+ * buffer u_buff_contr is zeroed.  get: the column count. */
+int qsp_set_delay_comp(qsp_solver* s, double delay);
+int qsp_get_delay_comp(qsp_solver* s, int32_t* cols);
+/* delay_buffer_sim (NMPC_controller.m:112-120): x (B x 4) advanced by delay_buff_comp Euler steps with
+ * the buffered inputs, oldest first -> x_sim (B x 4); and the buffer update the caller does after a
+ * solve, u_buff_contr = [u, u_buff_contr(:, 1:end-1)] (helper.m:255), u: B x 2. */
+int qsp_delay_buffer_sim(qsp_solver* s, const double* x, double* x_sim);
+int qsp_delay_buffer_push(qsp_solver* s, const double* u);
+/* the disturbance branch's contact re-projection alone: s = argmin |C(s) - (px, py)|^2 from s0 (per
+ * lane shape ids; fminunc in helper.m:230, restated as a damped Newton iteration) */
+int qsp_reproject_contact(qsp_solver* s, int32_t n, const int32_t* shape_id, const double* px, const double* py,
+                          const double* s0, double* s_out);
 
 /* ------------------------------------------------ device-resident fast path */
 int qsp_solve_device(qsp_solver* s, const qsp_device_io* io, void* hip_stream);

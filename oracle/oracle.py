@@ -175,7 +175,7 @@ class Oracle:
                             C.c_int(nthreads), _p(capped))
         return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
 
-    def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0):
+    def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0, delay_cols=0):
         """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place."""
         N = opts.N
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
@@ -192,8 +192,42 @@ class Oracle:
         self.L.or_controller_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
                                    C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]),
                                    _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                                   C.c_int(nthreads), _p(capped))
+                                   C.c_int(nthreads), _p(capped), C.c_int32(int(delay_cols)))
         return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
+
+    def closed_loop(self, opts, x0, traj, n_steps, index0=1, shape_id=None, noise=None, delay_cols=0,
+                    plant_delay_cols=0, dist_step=0, dist_amp=None, xwidth=None, nthreads=0):
+        """helper.m:195-322 closed loop (see or_closed_loop).  Returns X (nb, n+1, 4), Xsim (nb, n, 4),
+        U (nb, n, 2), status (nb, n)."""
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
+        nb, n = len(x0), int(n_steps)
+        sid = self._ids(shape_id, nb)
+        traj = np.ascontiguousarray(traj, np.float64).reshape(-1, 6)
+        idx = np.ascontiguousarray(np.broadcast_to(np.asarray(index0, np.int32), (nb,)), np.int32)
+        nz = None if noise is None else np.ascontiguousarray(noise, np.float64).reshape(n, nb, 4)
+        amp = np.ascontiguousarray(np.broadcast_to(np.asarray(0.0 if dist_amp is None else dist_amp, np.float64), (nb,)))
+        xw = np.ascontiguousarray(np.zeros(len(self._n)) if xwidth is None else np.asarray(xwidth, np.float64))
+        X = np.zeros((nb, n + 1, 4))
+        Xs = np.zeros((nb, n, 4))
+        U = np.zeros((nb, n, 2))
+        st = np.zeros((nb, n), np.int32)
+        r = self.L.or_closed_loop(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
+                                  C.c_int32(len(traj)), _p(idx), C.c_int32(n), None if nz is None else _p(nz),
+                                  C.c_int32(int(delay_cols)), C.c_int32(int(plant_delay_cols)), C.c_int32(int(dist_step)),
+                                  _p(amp), _p(xw), _p(X), _p(Xs), _p(U), _p(st), C.c_int(nthreads))
+        if r != 0:
+            raise ValueError("or_closed_loop: bad arguments")
+        return dict(X=X, Xsim=Xs, U=U, status=st)
+
+    def reproject_contact(self, px, py, s0, shape_id=None):
+        px = np.ascontiguousarray(px, np.float64).ravel()
+        n = len(px)
+        py = np.ascontiguousarray(np.broadcast_to(py, (n,)), np.float64)
+        s0 = np.ascontiguousarray(np.broadcast_to(s0, (n,)), np.float64)
+        sid = self._ids(shape_id, n)
+        s = np.zeros(n)
+        self.L.or_reproject_contact(*self._shape_args(), C.c_int32(n), _p(sid), _p(px), _p(py), _p(s0), _p(s))
+        return s
 
     @staticmethod
     def new_warm(nb, N):

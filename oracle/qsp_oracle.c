@@ -923,8 +923,86 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
     return 0;
 }
 
+/* Column c (1-based) of the controller's reference table as set_reference_trajectory builds it
+ * (NMPC_controller.m:425-431): D = delay_buff_comp zero columns prepended to the T columns of
+ * traj, whose u_t-reference row (6) copies the first real column; get_y_ref (:307-313) clamps
+ * an index past the end to the last column. */
+static void ref_column(const double *traj, int32_t T, int32_t D, int c, double out[6])
+{
+    if (c > T + D) c = T + D;
+    if (c < 1) c = 1;
+    if (c <= D) {
+        for (int q = 0; q < 5; ++q) out[q] = 0.0;
+        out[5] = traj[5];
+    } else {
+        for (int q = 0; q < 6; ++q) out[q] = traj[(size_t)(c - D - 1) * 6 + q];
+    }
+}
+
+/* One NMPC_controller.solve(x0, index_time) (NMPC_controller.m:329-423) on one lane.  Warm start
+ * X/U/PI + warm_valid in/out (shifted on return, :397-399); returns the status; u0 = U(:,1) of the
+ * unshifted solution (:403). */
+static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0_in[4], const double *traj,
+                           int32_t T, int32_t D, int32_t index_time, double *X, double *U, double *PI,
+                           uint8_t *warm_valid, double u0[2], int32_t *iters, int32_t *qp_iter, int32_t *qp_capped,
+                           double *cost, or_ws *ws)
+{
+    int N = o->N;
+    if (N < 1 || N > OR_MAX_N) return 1;
+    double yref[OR_MAX_N * 6], ye[4];
+    double x0[4];
+    memcpy(x0, x0_in, sizeof x0);
+    /* :332 pre-wrap of s into [-b, b) */
+    x0[3] = mat_mod(x0[3], sh->b) - sh->b * (x0[3] < 0.0 ? 1.0 : 0.0);
+    /* :343-348 reference staging with clamp (get_y_ref :307-313) */
+    for (int k = 0; k < N; ++k) ref_column(traj, T, D, index_time + k, yref + 6 * k);
+    for (int c = 0; c < 4; ++c) ye[c] = yref[6 * (N - 1) + c];
+    /* :351-355 cold start */
+    if (!*warm_valid) {
+        for (int q = 0; q < 4 * (N + 1); ++q) X[q] = 0.0;
+        for (int k = 0; k < N; ++k) { U[2 * k] = o->u_n_lb; U[2 * k + 1] = 0.0; }
+        for (int q = 0; q < 4 * N; ++q) PI[q] = 0.0;
+    }
+    /* :357-364 clip first control */
+    double vb = v_bound(sh, o, x0[3]);
+    if (fabs(U[1]) > vb) {
+        double ut_old = U[1];
+        U[1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
+        U[0] = U[1] * U[0] / ut_old;
+    }
+    /* :366-380 Euler warm-start rollout with per-stage clip */
+    memcpy(X, x0, sizeof x0);
+    for (int j = 1; j <= N; ++j) {
+        double f[4];
+        dynamics(sh, X + 4 * (j - 1), U + 2 * (j - 1), f, NULL);
+        for (int c = 0; c < 4; ++c) X[4 * j + c] = X[4 * (j - 1) + c] + o->Ts * f[c];
+        vb = v_bound(sh, o, X[4 * j + 3]);
+        if (j == N) break;
+        if (fabs(U[2 * j + 1]) > vb) {
+            double ut_old = U[2 * j + 1];
+            U[2 * j + 1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
+            U[2 * j] = U[2 * j + 1] * U[2 * j] / ut_old;
+        }
+    }
+    /* :389 solve */
+    ws->qp_total = 0;
+    ws->qp_capped = 0;
+    int status = sqp_solve(sh, o, x0, yref, ye, X, U, PI, NULL, iters, ws);
+    if (qp_iter) *qp_iter = ws->qp_total;
+    if (qp_capped) *qp_capped = ws->qp_capped;
+    if (cost) *cost = ocp_cost(o, N, X, U, yref, ye);
+    u0[0] = U[0]; u0[1] = U[1];
+    /* :397-399 shift (duplicate last column) */
+    memmove(U, U + 2, sizeof(double) * 2 * (N - 1));
+    memmove(X, X + 4, sizeof(double) * 4 * N);
+    memmove(PI, PI + 4, sizeof(double) * 4 * (N - 1));
+    *warm_valid = 1;
+    return status;
+}
+
 /* Batched NMPC_controller.solve(x0, index_time) (NMPC_controller.m:329-423).
- * traj: T x 6 reference table (column k = y_ref(:,k+1)), shared by all lanes.
+ * traj: T x 6 reference table (column k = y_ref(:,k+1)), shared by all lanes; delay_cols = the
+ * controller's delay_buff_comp (the table as set_reference_trajectory prepends it).
  * index_time: B (1-based, as in MATLAB).  Warm start Xw/Uw/PIw: B x ... in/out,
  * warm_valid: B flags (0 = cold start, :351-355); on return they hold the SHIFTED
  * solution (:397-399) and warm_valid = 1.  u0: B x 2 (the unshifted U(:,1), :403). */
@@ -933,7 +1011,7 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                         const double *x0_in, const double *traj, int32_t T, const int32_t *index_time,
                         double *Xw, double *Uw, double *PIw, uint8_t *warm_valid,
                         double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads,
-                        int32_t *qp_capped)
+                        int32_t *qp_capped, int32_t delay_cols)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -943,64 +1021,152 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
     #pragma omp parallel
     {
         or_ws *ws = (or_ws *)malloc(sizeof(or_ws));
-        double yref[OR_MAX_N * 6], ye[4];
         #pragma omp for schedule(dynamic, 1)
         for (int32_t i = 0; i < nb; ++i) {
             or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
-            double *X = Xw + (size_t)i * 4 * (N + 1), *U = Uw + (size_t)i * 2 * N, *PI = PIw + (size_t)i * 4 * N;
-            double x0[4];
-            memcpy(x0, x0_in + 4 * i, sizeof x0);
-            /* :332 pre-wrap of s into [-b, b) */
-            x0[3] = mat_mod(x0[3], sh.b) - sh.b * (x0[3] < 0.0 ? 1.0 : 0.0);
-            /* :343-348 reference staging with clamp (get_y_ref :307-313) */
-            for (int k = 0; k < N; ++k) {
-                int idx = index_time[i] + k;           /* 1-based */
-                if (idx > T) idx = T;
-                for (int c = 0; c < 6; ++c) yref[6 * k + c] = traj[(size_t)(idx - 1) * 6 + c];
-            }
-            for (int c = 0; c < 4; ++c) ye[c] = yref[6 * (N - 1) + c];
-            /* :351-355 cold start */
-            if (!warm_valid[i]) {
-                for (int q = 0; q < 4 * (N + 1); ++q) X[q] = 0.0;
-                for (int k = 0; k < N; ++k) { U[2 * k] = o->u_n_lb; U[2 * k + 1] = 0.0; }
-                for (int q = 0; q < 4 * N; ++q) PI[q] = 0.0;
-            }
-            /* :357-364 clip first control */
-            double vb = v_bound(&sh, o, x0[3]);
-            if (fabs(U[1]) > vb) {
-                double ut_old = U[1];
-                U[1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
-                U[0] = U[1] * U[0] / ut_old;
-            }
-            /* :366-380 Euler warm-start rollout with per-stage clip */
-            memcpy(X, x0, sizeof x0);
-            for (int j = 1; j <= N; ++j) {
-                double f[4];
-                dynamics(&sh, X + 4 * (j - 1), U + 2 * (j - 1), f, NULL);
-                for (int c = 0; c < 4; ++c) X[4 * j + c] = X[4 * (j - 1) + c] + o->Ts * f[c];
-                vb = v_bound(&sh, o, X[4 * j + 3]);
-                if (j == N) break;
-                if (fabs(U[2 * j + 1]) > vb) {
-                    double ut_old = U[2 * j + 1];
-                    U[2 * j + 1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
-                    U[2 * j] = U[2 * j + 1] * U[2 * j] / ut_old;
-                }
-            }
-            /* :389 solve */
-            ws->qp_total = 0;
-            ws->qp_capped = 0;
-            status[i] = sqp_solve(&sh, o, x0, yref, ye, X, U, PI, NULL, iters ? iters + i : NULL, ws);
-            if (qp_iter) qp_iter[i] = ws->qp_total;
-            if (qp_capped) qp_capped[i] = ws->qp_capped;
-            cost[i] = ocp_cost(o, N, X, U, yref, ye);
-            u0[2 * i] = U[0]; u0[2 * i + 1] = U[1];
-            /* :397-399 shift (duplicate last column) */
-            memmove(U, U + 2, sizeof(double) * 2 * (N - 1));
-            memmove(X, X + 4, sizeof(double) * 4 * N);
-            memmove(PI, PI + 4, sizeof(double) * 4 * (N - 1));
-            warm_valid[i] = 1;
+            status[i] = ctrl_solve_lane(&sh, o, x0_in + 4 * i, traj, T, delay_cols, index_time[i],
+                                        Xw + (size_t)i * 4 * (N + 1), Uw + (size_t)i * 2 * N, PIw + (size_t)i * 4 * N,
+                                        warm_valid + i, u0 + 2 * i, iters ? iters + i : NULL, qp_iter ? qp_iter + i : NULL,
+                                        qp_capped ? qp_capped + i : NULL, cost + i, ws);
         }
         free(ws);
+    }
+    return 0;
+}
+
+/* Contact re-projection after a lateral disturbance (helper.m:221-236): s minimising
+ * |C(s) - p|^2, p = (-xwidth/2, C_y(s_x) - amplitude), started from s0 (fminunc in the
+ * reference, whose iterates cannot be reproduced: restated as a damped Newton iteration on the
+ * periodic spline, C evaluated at the floor-mod of s as evalSpline does, bspline_shape.m:192-199;
+ * it converges to the local minimum of the start point's basin). */
+static double phi_contact(const or_shape *sh, double s, double px, double py)
+{
+    double C[2], dC[2];
+    spline_C(sh, mat_mod(s, sh->b), C, dC);
+    return (C[0] - px) * (C[0] - px) + (C[1] - py) * (C[1] - py);
+}
+
+static double reproject_contact(const or_shape *sh, double px, double py, double s0)
+{
+    double s = s0, phi = phi_contact(sh, s, px, py);
+    for (int it = 0; it < 60; ++it) {
+        double C[2], dC[2], D[2], dD[2];
+        const double sw = mat_mod(s, sh->b);
+        spline_C(sh, sw, C, dC);
+        spline_Cdot(sh, sw, D, dD);
+        const double ex = C[0] - px, ey = C[1] - py;
+        const double g = 2.0 * (ex * dC[0] + ey * dC[1]);
+        const double h = 2.0 * (dC[0] * dC[0] + dC[1] * dC[1] + ex * dD[0] + ey * dD[1]);
+        if (fabs(g) < 1e-14) break;
+        double step = h > 0.0 ? -g / h : (g > 0.0 ? -0.05 : 0.05) * sh->b;
+        const double smax = 0.25 * sh->b;
+        if (step > smax) step = smax;
+        if (step < -smax) step = -smax;
+        int ok = 0;
+        double sn = s, phin = phi;
+        for (int k = 0; k < 60; ++k) {
+            sn = s + step;
+            phin = phi_contact(sh, sn, px, py);
+            if (phin < phi) { ok = 1; break; }
+            step *= 0.5;
+        }
+        if (!ok) break;
+        s = sn;
+        phi = phin;
+        if (fabs(step) < 1e-13 * sh->b) break;
+    }
+    return s;
+}
+
+/* Batched closed loop of helper.m:195-322 (closed_loop_matlab) with NMPC_controller.solve:
+ * per step i = 1..n_steps: (disturbance at i == dist_step: y += amplitude, contact re-projected),
+ * sim_noise, the controller's delay prediction (delay_buffer_sim, NMPC_controller.m:112-120:
+ * delay_cols Euler steps with the buffered inputs, oldest first), u = solve(x_sim, index0 + i - 1 +
+ * delay_cols), the controller buffer push, then the plant x += Ts f(x, u) -- with plant_delay_cols
+ * > 0 the plant applies its buffered input (helper.m:289-296).  Cold start; both buffers start at
+ * zero.  Outputs: Xtraj nb x (n+1) x 4 (states after disturbance and noise), Xsim nb x n x 4 (the
+ * predicted states handed to the solver; optional), Utraj nb x n x 2, Straj nb x n (status). */
+int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
+                   int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id, const double *x0_in,
+                   const double *traj, int32_t T, const int32_t *index0, int32_t n_steps, const double *noise,
+                   int32_t delay_cols, int32_t plant_delay_cols, int32_t dist_step, const double *dist_amp,
+                   const double *xwidth, double *Xtraj, double *Xsim, double *Utraj, int32_t *Straj, int nthreads)
+{
+    int N = o->N;
+    if (N > OR_MAX_N || delay_cols < 0 || plant_delay_cols < 0 || delay_cols > 1024 || plant_delay_cols > 1024) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    #pragma omp parallel
+    {
+        or_ws *ws = (or_ws *)malloc(sizeof(or_ws));
+        double *X = (double *)malloc(sizeof(double) * 4 * (N + 1)), *U = (double *)malloc(sizeof(double) * 2 * N);
+        double *PI = (double *)malloc(sizeof(double) * 4 * N);
+        double *ubc = (double *)calloc(2 * (size_t)(delay_cols + 1), sizeof(double));
+        double *ubp = (double *)calloc(2 * (size_t)(plant_delay_cols + 1), sizeof(double));
+        #pragma omp for schedule(dynamic, 1)
+        for (int32_t i = 0; i < nb; ++i) {
+            or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
+            uint8_t valid = 0;
+            memset(ubc, 0, sizeof(double) * 2 * (size_t)(delay_cols + 1));
+            memset(ubp, 0, sizeof(double) * 2 * (size_t)(plant_delay_cols + 1));
+            double x[4];
+            memcpy(x, x0_in + 4 * i, sizeof x);
+            double s0_spline = 0.0;
+            for (int32_t t = 0; t < n_steps; ++t) {
+                if (dist_step > 0 && t + 1 == dist_step) {
+                    x[1] += dist_amp[i];
+                    double C[2], dC[2];
+                    spline_C(&sh, mat_mod(x[3], sh.b), C, dC);
+                    const double s = reproject_contact(&sh, -0.5 * xwidth[shape_id[i]], C[1] - dist_amp[i], s0_spline);
+                    s0_spline = mat_mod(s, sh.b) - sh.b * (s < 0.0 ? 1.0 : 0.0);
+                    x[3] = s0_spline;
+                }
+                if (noise)
+                    for (int c = 0; c < 4; ++c) x[c] += noise[((size_t)t * nb + i) * 4 + c];
+                memcpy(Xtraj + ((size_t)i * (n_steps + 1) + t) * 4, x, sizeof x);
+                double xs[4];
+                memcpy(xs, x, sizeof xs);
+                for (int k = 1; k <= delay_cols; ++k) {       /* u_buff_contr(:, end-k+1): oldest first */
+                    double f[4];
+                    dynamics(&sh, xs, ubc + 2 * (delay_cols - k), f, NULL);
+                    for (int c = 0; c < 4; ++c) xs[c] += o->Ts * f[c];
+                }
+                if (Xsim) memcpy(Xsim + ((size_t)i * n_steps + t) * 4, xs, sizeof xs);
+                double u[2];
+                const int st = ctrl_solve_lane(&sh, o, xs, traj, T, delay_cols, index0[i] + t + delay_cols, X, U, PI,
+                                               &valid, u, NULL, NULL, NULL, NULL, ws);
+                if (delay_cols > 0) {                         /* u_buff_contr = [u, u_buff_contr(:, 1:end-1)] */
+                    memmove(ubc + 2, ubc, sizeof(double) * 2 * (size_t)(delay_cols - 1));
+                    ubc[0] = u[0]; ubc[1] = u[1];
+                }
+                memcpy(Utraj + ((size_t)i * n_steps + t) * 2, u, sizeof u);
+                if (Straj) Straj[(size_t)i * n_steps + t] = st;
+                double f[4];
+                if (plant_delay_cols == 0) {
+                    dynamics(&sh, x, u, f, NULL);
+                } else {                                      /* u_buff_plant(:, end), then push */
+                    dynamics(&sh, x, ubp + 2 * (plant_delay_cols - 1), f, NULL);
+                    memmove(ubp + 2, ubp, sizeof(double) * 2 * (size_t)(plant_delay_cols - 1));
+                    ubp[0] = u[0]; ubp[1] = u[1];
+                }
+                for (int c = 0; c < 4; ++c) x[c] += o->Ts * f[c];
+            }
+            memcpy(Xtraj + ((size_t)i * (n_steps + 1) + n_steps) * 4, x, sizeof x);
+        }
+        free(ws); free(X); free(U); free(PI); free(ubc); free(ubp);
+    }
+    return 0;
+}
+
+/* contact re-projection alone (building block for the tests) */
+int or_reproject_contact(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
+                         int max_ctrl, int32_t n, const int32_t *shape_id, const double *px, const double *py,
+                         const double *s0, double *s)
+{
+    for (int32_t i = 0; i < n; ++i) {
+        or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
+        s[i] = reproject_contact(&sh, px[i], py[i], s0[i]);
     }
     return 0;
 }

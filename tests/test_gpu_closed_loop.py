@@ -125,3 +125,127 @@ def test_c_host_closed_loop(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     g = np.load(os.path.join(GOLDEN, "config1_rti_full.npz"))
     np.testing.assert_allclose(np.loadtxt(out), g["U"], rtol=0, atol=1e-8)
+
+
+XWIDTH = {"santal": 0.068, "balea": 0.071, "montana": 0.057, "pulirapid": 0.13}   # object_selection.m
+
+
+def _cl_setup(nb, N, K, seed):
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    x0 = config2_x0(nb, seed)
+    sid = np.arange(nb) % 4
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K)
+    s.set_shapes([make_shape(n) for n in NAMES], shape_id=sid)
+    s.set_reference_trajectory(straight_traj())
+    return s, x0, sid
+
+
+def _stable_lanes(oracle, run, x0):
+    ref = run(x0)
+    st = np.ones(len(x0), bool)
+    for f in (1e-13, -1e-13):
+        rp = run(x0 * (1 + f))
+        st &= np.abs(rp["U"] - ref["U"]).max(axis=(1, 2)) < 1e-9
+    return ref, st
+
+
+@pytest.mark.parametrize("delay,plant_delay", [(0.1, 0.0), (0.1, 0.1), (0.0, 0.15), (0.35, 0.35)])
+def test_closed_loop_delay_matches_oracle(oracle, delay, plant_delay):
+    """A17 + helper.m's plant delay: set_delay_comp (delay_buff_comp = ceil(delay/Ts) prefix columns,
+    delay_buffer_sim with the buffered inputs, oldest first) and the plant's u_buff_plant, on the
+    device closed loop, against the oracle's or_closed_loop (helper.m:195-322 restated)."""
+    from oracle.oracle import make_opts
+    N, nb, K, T = 20, 32, 2, 14
+    s, x0, sid = _cl_setup(nb, N, K, 41)
+    s.set_delay_comp(delay)
+    D = s.delay_cols()
+    Dp = int(np.ceil(plant_delay / 0.05))
+    assert D == int(np.ceil(delay / 0.05))
+    r = s.closed_loop(x0, T, plant_delay=plant_delay)
+    s.close()
+    op = make_opts(N=N, sqp_iters=K)
+    run = lambda x: oracle.closed_loop(op, x, straight_traj(), T, shape_id=sid, delay_cols=D,  # noqa: E731
+                                       plant_delay_cols=Dp)
+    ref, st = _stable_lanes(oracle, run, x0)
+    assert st.mean() > 0.5, st.mean()
+    np.testing.assert_array_equal(r["status"][st], ref["status"][st])
+    assert np.abs(r["U"] - ref["U"]).max(axis=(1, 2))[st].max() < 1e-6
+    assert np.abs(r["X"] - ref["X"]).max(axis=(1, 2))[st].max() < 1e-8
+    assert np.abs(r["Xsim"] - ref["Xsim"]).max(axis=(1, 2))[st].max() < 1e-8
+    if D > 0:   # the prediction moved the state (the buffer held earlier inputs)
+        assert np.abs(r["Xsim"][:, D + 1:] - r["X"][:, D + 1:-1]).max() > 1e-6
+
+
+def test_closed_loop_disturbance_matches_oracle(oracle):
+    """helper.m:221-236: at step t_dist, y += amplitude and the contact point is re-projected onto
+    the contour (s nearest to (-xwidth/2, C_y(s) - amplitude), from s0 = 0); then the loop goes on."""
+    from oracle.oracle import make_opts
+    N, nb, K, T, td = 20, 24, 2, 10, 4
+    s, x0, sid = _cl_setup(nb, N, K, 43)
+    amp = np.linspace(-0.02, 0.02, nb)
+    r = s.closed_loop(x0, T, disturbance=True, t_dist=td, amplitude=amp)
+    s.close()
+    op = make_opts(N=N, sqp_iters=K)
+    xw = [XWIDTH[n] for n in NAMES]
+    run = lambda x: oracle.closed_loop(op, x, straight_traj(), T, shape_id=sid, dist_step=td,  # noqa: E731
+                                       dist_amp=amp, xwidth=xw)
+    ref, st = _stable_lanes(oracle, run, x0)
+    assert st.mean() > 0.5, st.mean()
+    # the disturbed state itself (step td, before the solve) on every lane: x, y, theta exactly as
+    # the oracle; the re-projected s to 1e-6 (a target near a circular arc's centre makes the
+    # minimiser flat: the two spline formulations then stop a little apart)
+    np.testing.assert_allclose(r["X"][:, td - 1, :3], ref["X"][:, td - 1, :3], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(r["X"][:, td - 1, 3], ref["X"][:, td - 1, 3], rtol=0, atol=1e-6)
+    assert np.abs(r["U"] - ref["U"]).max(axis=(1, 2))[st].max() < 1e-6
+    assert np.abs(r["X"] - ref["X"]).max(axis=(1, 2))[st].max() < 1e-8
+    # the re-projected s is wrapped into [-b, b) (helper.m:233)
+    b = oracle.tab["params"][sid, 0]
+    assert np.all(np.abs(r["X"][:, td - 1, 3]) <= b)
+
+
+def test_reproject_contact_matches_oracle(oracle):
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    gpu = OcpSolver(N=10, batch=1)
+    gpu.set_shapes([make_shape(n) for n in NAMES])
+    rng = np.random.default_rng(9)
+    n = 400
+    sid = rng.integers(0, 4, n)
+    b = oracle.tab["params"][sid, 0]
+    s_true = rng.uniform(0, 1, n) * b
+    C = oracle.spline(s_true, sid)[0]
+    px = C[:, 0] + rng.normal(0, 2e-3, n)
+    py = C[:, 1] + rng.normal(0, 2e-3, n)
+    s0 = s_true + rng.uniform(-0.02, 0.02, n)
+    so = oracle.reproject_contact(px, py, s0, sid)
+    sg = gpu.reproject_contact(px, py, s0, sid)
+    gpu.close()
+    np.testing.assert_allclose(sg, so, rtol=0, atol=1e-8)
+    # stationary point of |C(s) - p|^2: the tangent is orthogonal to C(s) - p
+    Cs, dCs, D, dD, _ = oracle.spline(np.mod(so, b), sid)
+    g = (Cs[:, 0] - px) * D[:, 0] + (Cs[:, 1] - py) * D[:, 1]
+    assert np.abs(g).max() < 1e-10
+
+
+def test_delay_buffer_mirror(oracle):
+    """NMPC_controller.delay_buffer_sim + the helper's buffer push through the controller mirror."""
+    from uclv_qs_pushing_matlab_amd.controller import NMPCController
+    from uclv_qs_pushing_matlab_amd.model import PusherSliderModel
+    from uclv_qs_pushing_matlab_amd.objects import object_selection
+    plant = PusherSliderModel("real_plant", object_selection("santal"), 0.0, object_name="santal")
+    c = NMPCController("nmpc", plant, 0.05, 10, batch=3, nlp_solver_type="SQP_RTI", sqp_iters=2)
+    c.create_ocp_solver()
+    c.set_delay_comp(0.12)
+    assert c.delay_buff_comp == 3
+    x = config2_x0(3, 5)
+    np.testing.assert_array_equal(c.delay_buffer_sim(plant, x), x)        # empty buffer: zero inputs, f(x, 0) = 0
+    us = [np.array([[0.01, 0.002]] * 3) * (k + 1) for k in range(4)]
+    for u in us:
+        c.push_u_buffer(u)
+    xs = c.delay_buffer_sim(plant, x)
+    ref = x.copy()
+    for u in (us[1], us[2], us[3]):                                       # oldest of the 3 kept first
+        f, _ = oracle.dynamics(ref, u)
+        ref = ref + 0.05 * f
+    np.testing.assert_allclose(xs, ref, rtol=0, atol=1e-12)

@@ -163,10 +163,10 @@ def test_stage0_s_bound_infeasible(oracle):
         ok[[2, 5]] = False        # with the option off their QPs are infeasible from stage 1 on: junk iterates
         np.testing.assert_array_equal(res[on][1][ok], r["status"][ok])
         np.testing.assert_array_equal(res[on][2][ok], r["iters"][ok])
-        np.testing.assert_allclose(u[ok], r["u0"][ok], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(u[ok], r["u0"][ok], rtol=0, atol=1e-5)   # K = 5 full steps
         if on:
             np.testing.assert_array_equal(res[on][1], r["status"])
-            np.testing.assert_allclose(u, r["u0"], rtol=0, atol=1e-6)   # lanes 2, 5: the initial guess
+            np.testing.assert_allclose(u[[2, 5]], r["u0"][[2, 5]], rtol=0, atol=1e-12)   # the initial guess
     u, st, it = res[True]
     assert list(np.where(st != 0)[0]) == [2, 5] and np.all(st[[2, 5]] == 4) and np.all(it[[2, 5]] == 0)
     assert np.all(res[False][1] == 0)

@@ -288,3 +288,37 @@ def test_main_m_sqp_closed_loop_golden(oracle):
         fx, _ = oracle.dynamics(xs, r["u0"])
         xs = xs + 0.05 * fx
     assert np.mean(g["status"] == 0) > 0.8 and abs(xs[0, 0] - 0.1) < 2e-3
+
+
+def test_reference_table_prefix_and_closed_loop_composition(oracle):
+    """set_reference_trajectory with delay_buff_comp D (NMPC_controller.m:425-431): D zero columns
+    prepended, the u_t-reference row copied from the first real column; the oracle's closed loop
+    equals the step-by-step composition of controller_solve + Euler plant (helper.m:195-322) when
+    no delay is set, and with D > 0 the solve at step i reads column i + D (= the original i)."""
+    traj = straight_traj()
+    traj[:, 5] = 0.003
+    N, nb, T = 10, 4, 6
+    x0 = config2_x0(nb, 2)
+    sid = np.arange(nb) % 4
+    op = make_opts(N=N, sqp_iters=2)
+    # prefix columns: index 1 with D = 3 reads columns 1..3 of the prefix, then the table
+    w1, w2 = oracle.new_warm(nb, N), oracle.new_warm(nb, N)
+    pre = np.zeros((3 + len(traj), 6))
+    pre[3:] = traj
+    pre[:3, 5] = traj[0, 5]
+    a = oracle.controller_solve(op, x0, traj, 1, w1, shape_id=sid, delay_cols=3)
+    b = oracle.controller_solve(op, x0, pre, 1, w2, shape_id=sid)
+    np.testing.assert_array_equal(a["u0"], b["u0"])
+    r = oracle.closed_loop(op, x0, traj, T, shape_id=sid)
+    w = oracle.new_warm(nb, N)
+    x = x0.copy()
+    for t in range(T):
+        ro = oracle.controller_solve(op, x, traj, 1 + t, w, shape_id=sid)
+        np.testing.assert_array_equal(ro["u0"], r["U"][:, t])
+        f, _ = oracle.dynamics(x, ro["u0"], sid)
+        x = x + 0.05 * f
+    np.testing.assert_array_equal(x, r["X"][:, -1])
+    # delay D: the first solve sees x advanced by D steps of zero input (= x, f(x, 0) = 0) and the
+    # original columns, so it equals the undelayed first step
+    rd = oracle.closed_loop(op, x0, traj, 2, shape_id=sid, delay_cols=2)
+    np.testing.assert_array_equal(rd["U"][:, 0], r["U"][:, 0])

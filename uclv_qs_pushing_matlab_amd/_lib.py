@@ -39,8 +39,13 @@ class Shape(C.Structure):
         ("n_ctrl", C.c_int32), ("pad_", C.c_int32),
         ("ctrl", (C.c_double * 2) * MAX_CTRL),
         ("knots", C.c_double * (MAX_CTRL + 4)),
-        ("b", C.c_double), ("c_ellipse", C.c_double), ("mu_sp", C.c_double),
+        ("b", C.c_double), ("c_ellipse", C.c_double), ("mu_sp", C.c_double), ("xwidth", C.c_double),
     ]
+
+
+class ClosedLoopOpts(C.Structure):
+    _fields_ = [("plant_delay", C.c_double), ("disturbance", C.c_int32), ("t_dist", C.c_int32),
+                ("amplitude", C.c_void_p)]
 
 
 class DeviceIO(C.Structure):
@@ -88,6 +93,12 @@ _SIGS = {
     "qsp_controller_solve": [_P, _P, _P],
     "qsp_controller_reset": [_P],
     "qsp_closed_loop": [_P, _P, _P, _I, _P, _P, _P, _P],
+    "qsp_closed_loop_ex": [_P, C.POINTER(ClosedLoopOpts), _P, _P, _I, _P, _P, _P, _P, _P],
+    "qsp_set_delay_comp": [_P, _D],
+    "qsp_get_delay_comp": [_P, C.POINTER(_I)],
+    "qsp_delay_buffer_sim": [_P, _P, _P],
+    "qsp_delay_buffer_push": [_P, _P],
+    "qsp_reproject_contact": [_P, _I, _P, _P, _P, _P, _P],
     "qsp_solve_device": [_P, C.POINTER(DeviceIO), _P],
     "qsp_synchronize": [_P],
     "qsp_set_stream_parts": [_P, _I],

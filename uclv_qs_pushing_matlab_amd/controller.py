@@ -75,14 +75,22 @@ class NMPCController:
         self._push_ctrl_params()
 
     def set_delay_comp(self, delay):                                       # :106-110
-        if delay != 0:
-            raise NotImplementedError("delay compensation is inactive in every reference configuration "
-                                      "(main.m:74-75); only delay = 0 is supported")
-        self.delay_compensation = delay
-        self.delay_buff_comp = 0
+        """delay_buff_comp = ceil(delay / Ts); the per-lane input buffer u_buff_contr (device) starts at
+        zero; the reference table is read with the delay_buff_comp prefix columns (:425-431)."""
+        if self.ocp_solver is None:
+            raise RuntimeError("create_ocp_solver before set_delay_comp")
+        self.ocp_solver.set_delay_comp(delay)
+        self.delay_compensation = float(delay)
+        self.delay_buff_comp = self.ocp_solver.delay_cols()
 
-    def delay_buffer_sim(self, plant, x):                                  # :112-120 (no-op at delay 0)
-        return np.asarray(x, np.float64)
+    def delay_buffer_sim(self, plant, x):                                  # :112-120
+        """x predicted delay_buff_comp steps ahead with the buffered inputs (oldest first)."""
+        return self.ocp_solver.delay_buffer_sim(np.broadcast_to(np.asarray(x, np.float64).reshape(-1, 4),
+                                                                (self.batch, 4)))
+
+    def push_u_buffer(self, u):
+        """u_buff_contr = [u, u_buff_contr(:, 1:end-1)] -- the update helper.m:255 performs."""
+        self.ocp_solver.delay_buffer_push(np.broadcast_to(np.asarray(u, np.float64).reshape(-1, 2), (self.batch, 2)))
 
     def update_constraints(self, u_n_ub, u_t_ub, u_n_lb, u_t_lb):          # :122-142
         self.u_n_lb, self.u_n_ub, self.u_t_lb, self.u_t_ub = u_n_lb, u_n_ub, u_t_lb, u_t_ub

@@ -56,6 +56,10 @@ struct qsp_solver {
     int n_shapes = 0;
     DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, qp_capped, cost;
     DevBuf warm_valid, traj, index_time;
+    // delay compensation (set_delay_comp, NMPC_controller.m:106-110): delay_buff_comp columns and the
+    // per-lane controller input buffer u_buff_contr (B x D x 2, column 0 newest); closed-loop state
+    int32_t D = 0;
+    DevBuf ubc, ubp, cl_x, cl_xsim, cl_amp;
     DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit, whist;
     DevBuf scratch[12];
     int32_t T = 0;
@@ -242,16 +246,24 @@ static int check_ids(qsp_solver* s, int32_t n, const int32_t* ids) {
 }
 
 __global__ void stage_yref_kernel(const double* traj, int T, int per_lane, const int32_t* index_time, int offset,
-                                  int B, int N, double* yref, double* yref_e) {
+                                  int D, int B, int N, double* yref, double* yref_e) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     if (per_lane) traj += (size_t)i * T * 6;
-    // get_y_ref (NMPC_controller.m:307-313): column index_time+k (1-based), clamped to the last
+    // get_y_ref (NMPC_controller.m:307-313): column index_time+k (1-based) of the table as
+    // set_reference_trajectory (:425-431) builds it -- D = delay_buff_comp zero columns prepended,
+    // their u_t-reference row copied from the first real column -- clamped to the last column
     for (int k = 0; k < N; ++k) {
         int idx = index_time[i] + offset + k;
-        if (idx > T) idx = T;
+        if (idx > T + D) idx = T + D;
         if (idx < 1) idx = 1;
-        for (int c = 0; c < 6; ++c) yref[((size_t)i * N + k) * 6 + c] = traj[(size_t)(idx - 1) * 6 + c];
+        double* out = yref + ((size_t)i * N + k) * 6;
+        if (idx <= D) {
+            for (int c = 0; c < 5; ++c) out[c] = 0.0;
+            out[5] = traj[5];
+        } else {
+            for (int c = 0; c < 6; ++c) out[c] = traj[(size_t)(idx - D - 1) * 6 + c];
+        }
     }
     // terminal reference = last stage reference (:348)
     for (int c = 0; c < 4; ++c) yref_e[(size_t)i * 4 + c] = yref[((size_t)i * N + N - 1) * 6 + c];
@@ -262,7 +274,7 @@ static hipError_t launch_controller_step(qsp_solver* s, int offset) {
     const size_t B = s->o.batch;
     hipLaunchKernelGGL(stage_yref_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s->stream,
                        s->traj.as<double>(), s->T, s->traj_per_lane ? 1 : 0, s->index_time.as<int32_t>(), offset,
-                       (int)B, s->o.N,
+                       s->D, (int)B, s->o.N,
                        s->yref.as<double>(), s->yref_e.as<double>());
     return hipGetLastError();
 }
@@ -426,7 +438,8 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
 int qsp_destroy(qsp_solver* s) {
     if (!s) return QSP_OK;
     (void)hipSetDevice(s->o.device);
-    DevBuf* bufs[] = {&s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
+    DevBuf* bufs[] = {&s->ubc, &s->ubp, &s->cl_x, &s->cl_xsim, &s->cl_amp,
+                      &s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->qp_capped, &s->cost,
                       &s->warm_valid,
                       &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
@@ -529,6 +542,7 @@ int qsp_set_shapes(qsp_solver* s, const qsp_shape* shapes, int32_t n) {
         for (int i = 0; i < nc; ++i) { d.ctrl[2 * i] = in.ctrl[i][0]; d.ctrl[2 * i + 1] = in.ctrl[i][1]; }
         const double h0 = in.knots[4] - in.knots[3];
         d.inv_h = h0 > 0.0 ? 1.0 / h0 : 0.0;
+        d.xwidth = in.xwidth;
         // derivative-spline coefficients (bspline_shape.m:92-99 with zero-denominator guard :93)
         for (int i = 1; i < nc; ++i) {
             const double den = d.knots[i + 3] - d.knots[i];
@@ -732,47 +746,169 @@ int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_t
     return run_timed(s, controller_args(s));
 }
 
-int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int32_t n_steps, const double* noise,
-                    double* X_traj, double* U_traj, int32_t* status_traj) {
+// ------------------------------------------------------- delay compensation
+int qsp_set_delay_comp(qsp_solver* s, double delay) {
+    if (!s || !(delay >= 0.0)) return fail(QSP_ERR_ARG, "qsp_set_delay_comp: delay must be >= 0");
+    const double cols = std::ceil(delay / s->o.Ts);   // delay_buff_comp = ceil(delay / sample_time) (:108)
+    if (cols > 4096.0) return fail(QSP_ERR_ARG, "qsp_set_delay_comp: more than 4096 delay samples");
+    HIPCHK(hipSetDevice(s->o.device));
+    s->D = (int32_t)cols;
+    const size_t bytes = (size_t)s->o.batch * (size_t)(s->D > 0 ? s->D : 1) * 2 * 8;
+    HIPCHK(s->ubc.ensure(bytes));
+    HIPCHK(hipMemsetAsync(s->ubc.p, 0, bytes, s->stream));   // u_buff_contr = zeros (:109)
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_get_delay_comp(qsp_solver* s, int32_t* cols) {
+    if (!s || !cols) return fail(QSP_ERR_ARG, "qsp_get_delay_comp: null argument");
+    *cols = s->D;
+    return QSP_OK;
+}
+
+static ClosedLoopArgs cl_args(qsp_solver* s) {
+    ClosedLoopArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.shapes = s->shapes.as<ShapeDev>();
+    a.n_shapes = s->n_shapes;
+    a.sid = s->shape_id.as<int32_t>();
+    a.B = s->o.batch;
+    a.Ts = s->o.Ts;
+    a.D = s->D;
+    a.ubc = s->ubc.as<double>();
+    return a;
+}
+
+int qsp_delay_buffer_sim(qsp_solver* s, const double* x, double* x_sim) {
+    if (!s || !x || !x_sim) return fail(QSP_ERR_ARG, "qsp_delay_buffer_sim: null argument");
+    if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_delay_buffer_sim: no shapes set");
+    const size_t B = s->o.batch;
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(s->cl_x.ensure(B * 4 * 8));
+    HIPCHK(s->cl_xsim.ensure(B * 4 * 8));
+    HIPCHK(hipMemcpyAsync(s->cl_x.p, x, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
+    ClosedLoopArgs a = cl_args(s);
+    a.x = s->cl_x.as<double>();
+    a.xs = s->cl_xsim.as<double>();
+    HIPCHK(launch_delay_sim(a, s->stream));
+    HIPCHK(hipMemcpyAsync(x_sim, s->cl_xsim.p, B * 4 * 8, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_delay_buffer_push(qsp_solver* s, const double* u) {
+    if (!s || !u) return fail(QSP_ERR_ARG, "qsp_delay_buffer_push: null argument");
+    if (s->D == 0) return QSP_OK;
+    const size_t B = s->o.batch, D = (size_t)s->D;
+    std::vector<double> h(B * D * 2);
+    HIPCHK(hipSetDevice(s->o.device));
+    HIPCHK(hipMemcpyAsync(h.data(), s->ubc.p, h.size() * 8, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    for (size_t i = 0; i < B; ++i) {   // u_buff_contr = [u, u_buff_contr(:, 1:end-1)]  (helper.m:255)
+        double* b = h.data() + i * D * 2;
+        std::memmove(b + 2, b, (D - 1) * 2 * 8);
+        b[0] = u[2 * i];
+        b[1] = u[2 * i + 1];
+    }
+    HIPCHK(hipMemcpyAsync(s->ubc.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_closed_loop_ex(qsp_solver* s, const qsp_closed_loop_opts* o, const double* x0, const int32_t* index0,
+                       int32_t n_steps, const double* noise, double* X_traj, double* X_sim, double* U_traj,
+                       int32_t* status_traj) {
     if (!s || !x0 || !index0 || !X_traj || !U_traj || n_steps < 1)
         return fail(QSP_ERR_ARG, "qsp_closed_loop: bad argument");
     if (!s->have_traj) return fail(QSP_ERR_STATE, "qsp_closed_loop: no reference trajectory");
     if (s->n_shapes < 1) return fail(QSP_ERR_STATE, "qsp_closed_loop: no shapes set");
+    const double plant_delay = o ? o->plant_delay : 0.0;
+    if (!(plant_delay >= 0.0) || std::ceil(plant_delay / s->o.Ts) > 4096.0)
+        return fail(QSP_ERR_ARG, "qsp_closed_loop: plant_delay must be in [0, 4096 Ts]");
+    if (o && o->disturbance && o->t_dist < 1) return fail(QSP_ERR_ARG, "qsp_closed_loop: t_dist must be >= 1");
     const size_t B = s->o.batch, T = (size_t)n_steps;
+    const int Dp = (int)std::ceil(plant_delay / s->o.Ts);   // delay_buff_plant (helper.m:211)
     HIPCHK(hipSetDevice(s->o.device));
     DevBuf& dX = s->scratch[9];
     DevBuf& dU = s->scratch[10];
     DevBuf& dS = s->scratch[11];
     DevBuf& dN = s->scratch[3];
+    DevBuf& dXs = s->scratch[4];
     HIPCHK(dX.ensure(B * (T + 1) * 4 * 8));
     HIPCHK(dU.ensure(B * T * 2 * 8));
     HIPCHK(dS.ensure(B * T * 4));
+    if (X_sim) HIPCHK(dXs.ensure(B * T * 4 * 8));
     if (noise) HIPCHK(dN.ensure(T * B * 4 * 8));
+    HIPCHK(s->cl_x.ensure(B * 4 * 8));
+    HIPCHK(s->ubp.ensure(B * (size_t)(Dp > 0 ? Dp : 1) * 2 * 8));
+    if (s->D > 0) HIPCHK(s->ubc.ensure(B * (size_t)s->D * 2 * 8));
     HIPCHK(s->index_time.ensure(B * 4));
-    HIPCHK(hipMemcpyAsync(s->x0.p, x0, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->cl_x.p, x0, B * 4 * 8, hipMemcpyHostToDevice, s->stream));
     HIPCHK(hipMemcpyAsync(s->index_time.p, index0, B * 4, hipMemcpyHostToDevice, s->stream));
     if (noise) HIPCHK(hipMemcpyAsync(dN.p, noise, T * B * 4 * 8, hipMemcpyHostToDevice, s->stream));
-    // initial_condition_update -> clear_variables: the first solve is a cold start (main.m:79)
+    const bool dist = o && o->disturbance;
+    if (dist && o->amplitude) {
+        HIPCHK(s->cl_amp.ensure(B * 8));
+        HIPCHK(hipMemcpyAsync(s->cl_amp.p, o->amplitude, B * 8, hipMemcpyHostToDevice, s->stream));
+    }
+    // initial_condition_update -> clear_variables: the first solve is a cold start (main.m:79);
+    // both input buffers start at zero (set_delay_comp / closed_loop_matlab's u_buff_plant)
     HIPCHK(hipMemsetAsync(s->warm_valid.p, 0, B, s->stream));
-    const double* nz = noise ? dN.as<double>() : nullptr;
-    HIPCHK(launch_closed_loop_init((int)B, s->x0.as<double>(), nz, dX.as<double>(), n_steps, s->stream));
+    if (s->D > 0) HIPCHK(hipMemsetAsync(s->ubc.p, 0, B * (size_t)s->D * 2 * 8, s->stream));
+    if (Dp > 0) HIPCHK(hipMemsetAsync(s->ubp.p, 0, B * (size_t)Dp * 2 * 8, s->stream));
+    ClosedLoopArgs c = cl_args(s);
+    c.n_steps = n_steps;
+    c.x = s->cl_x.as<double>();
+    c.xs = s->x0.as<double>();                 // the solver's x0 (constr_x0)
+    c.noise = noise ? dN.as<double>() : nullptr;
+    c.dist_step = dist ? o->t_dist : 0;
+    c.dist_amp = (dist && o->amplitude) ? s->cl_amp.as<double>() : nullptr;
+    c.Dp = Dp;
+    c.ubp = s->ubp.as<double>();
+    c.u0 = s->u0.as<double>();
+    c.status = s->status.as<int32_t>();
+    c.Xtraj = dX.as<double>();
+    c.Xsim = X_sim ? dXs.as<double>() : nullptr;
+    c.Utraj = dU.as<double>();
+    c.Straj = dS.as<int32_t>();
     HIPCHK(hipEventRecord(s->ev0, s->stream));
     const SolveArgs a = controller_args(s);
     for (int32_t t = 0; t < n_steps; ++t) {
-        HIPCHK(launch_controller_step(s, t));                                  // y_ref for index0 + t
+        HIPCHK(launch_closed_loop_pre(c, t, s->stream));                       // disturbance, noise, delay_buffer_sim
+        HIPCHK(launch_controller_step(s, t + s->D));                           // y_ref for index0 + t + D
         HIPCHK(launch_sqp(a, s->S, s->stream, take_kernel_events(s), sqp_split(s)));   // NMPC_controller.solve
-        HIPCHK(launch_plant(s->shapes.as<ShapeDev>(), s->n_shapes, s->shape_id.as<int32_t>(), (int)B, s->o.Ts,
-                            s->x0.as<double>(),
-                            s->u0.as<double>(), s->status.as<int32_t>(), t, n_steps,
-                            (nz && t + 1 < n_steps) ? nz + (size_t)(t + 1) * B * 4 : nullptr, dX.as<double>(),
-                            dU.as<double>(), dS.as<int32_t>(), s->stream));
+        HIPCHK(launch_plant(c, t, s->stream));                                 // buffers, plant step, logs
     }
     HIPCHK(hipEventRecord(s->ev1, s->stream));
     HIPCHK(hipMemcpyAsync(X_traj, dX.p, B * (T + 1) * 4 * 8, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipMemcpyAsync(U_traj, dU.p, B * T * 2 * 8, hipMemcpyDeviceToHost, s->stream));
+    if (X_sim) HIPCHK(hipMemcpyAsync(X_sim, dXs.p, B * T * 4 * 8, hipMemcpyDeviceToHost, s->stream));
     if (status_traj) HIPCHK(hipMemcpyAsync(status_traj, dS.p, B * T * 4, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
     HIPCHK(hipEventElapsedTime(&s->last_ms, s->ev0, s->ev1));
+    return QSP_OK;
+}
+
+int qsp_closed_loop(qsp_solver* s, const double* x0, const int32_t* index0, int32_t n_steps, const double* noise,
+                    double* X_traj, double* U_traj, int32_t* status_traj) {
+    return qsp_closed_loop_ex(s, nullptr, x0, index0, n_steps, noise, X_traj, nullptr, U_traj, status_traj);
+}
+
+int qsp_reproject_contact(qsp_solver* s, int32_t n, const int32_t* sid, const double* px, const double* py,
+                          const double* s0, double* s_out) {
+    if (!s || n < 1 || !sid || !px || !py || !s0 || !s_out) return fail(QSP_ERR_ARG, "qsp_reproject_contact: bad argument");
+    int r = check_ids(s, n, sid);
+    if (r) return r;
+    HIPCHK(hipSetDevice(s->o.device));
+    auto& sc = s->scratch;
+    if ((r = stage_in(s, sc[0], sid, n)) || (r = stage_in(s, sc[1], px, n)) || (r = stage_in(s, sc[2], py, n)) ||
+        (r = stage_in(s, sc[5], s0, n)))
+        return r;
+    HIPCHK(sc[6].ensure((size_t)n * 8));
+    HIPCHK(launch_reproject(s->shapes.as<ShapeDev>(), s->n_shapes, sc[0].as<int32_t>(), n, sc[1].as<double>(),
+                            sc[2].as<double>(), sc[5].as<double>(), sc[6].as<double>(), s->stream));
+    if ((r = stage_out(s, s_out, sc[6], (size_t)n))) return r;
+    HIPCHK(hipStreamSynchronize(s->stream));
     return QSP_OK;
 }
 

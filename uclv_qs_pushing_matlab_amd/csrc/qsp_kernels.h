@@ -85,11 +85,33 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
 int sqp_parts_auto(int B, int N, int S, int cus);
 int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus);
 hipError_t launch_qp(const SolveArgs& a, int S, hipStream_t stream);   // one QP step on prepared workspace
-hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
-                                   hipStream_t stream);
-hipError_t launch_plant(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
-                        const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
-                        double* Xtraj, double* Utraj, int32_t* Straj, hipStream_t stream);
+// Device closed loop (helper.m:195-322): buffers and logs of qsp_closed_loop, one thread per lane.
+struct ClosedLoopArgs {
+    const ShapeDev* shapes;
+    int32_t n_shapes;
+    const int32_t* sid;        // B (nullptr: shape 0)
+    int32_t B, n_steps;
+    double Ts;
+    double* x;                 // B x 4   plant state
+    double* xs;                // B x 4   state handed to the solver (after the delay prediction)
+    const double* noise;       // n_steps x B x 4 (sim_noise) or nullptr
+    int32_t dist_step;         // 1-based step of the disturbance (0: none)
+    const double* dist_amp;    // B amplitude_dist (nullptr: 0)
+    int32_t D, Dp;             // controller delay_buff_comp, plant delay_buff_plant
+    double* ubc;               // B x D x 2  u_buff_contr (column 0 = newest)
+    double* ubp;               // B x Dp x 2 u_buff_plant
+    const double* u0;          // B x 2   the solve's u0
+    const int32_t* status;     // B
+    double* Xtraj;             // B x (n_steps + 1) x 4
+    double* Xsim;              // B x n_steps x 4 or nullptr
+    double* Utraj;             // B x n_steps x 2
+    int32_t* Straj;            // B x n_steps or nullptr
+};
+hipError_t launch_closed_loop_pre(const ClosedLoopArgs& a, int t, hipStream_t stream);
+hipError_t launch_plant(const ClosedLoopArgs& a, int t, hipStream_t stream);
+hipError_t launch_delay_sim(const ClosedLoopArgs& a, hipStream_t stream);   // x -> xs (delay_buffer_sim)
+hipError_t launch_reproject(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int n, const double* px,
+                            const double* py, const double* s0, double* s, hipStream_t stream);
 hipError_t launch_straight_lines(int B, int T, const double* x0, const double* xf, double t0, double tf, double Ts,
                                  int auto_angle, double* traj, hipStream_t stream);
 hipError_t launch_spline(const ShapeDev* shapes, const int32_t* sid, int n, const double* s, double* C, double* D,

@@ -1667,53 +1667,164 @@ __global__ void epilogue_kernel(SolveArgs A) {
 }
 
 // ------------------------------------------------------- closed-loop plant
-// helper.m:195-322 (closed_loop_matlab): sim_noise perturbation of x(:,i) before the solve,
-// plant x(:,i+1) = x(:,i) + Ts * evalModelVariableShape(x(:,i), u(:,i)) (:292-307), and the
-// trajectory / found_sol (status) logs.  One thread per lane.
-__global__ void closed_loop_init_kernel(int B, double* x, const double* noise0, double* Xtraj, int n_steps) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
-    for (int c = 0; c < 4; ++c) {
-        const double v = x[(size_t)i * 4 + c] + (noise0 ? noise0[(size_t)i * 4 + c] : 0.0);
-        x[(size_t)i * 4 + c] = v;
-        Xtraj[((size_t)i * (n_steps + 1)) * 4 + c] = v;
-    }
+// helper.m:195-322 (closed_loop_matlab), one thread per lane, around each NMPC_controller.solve:
+//   closed_loop_pre_kernel: the disturbance (:221-236), sim_noise (:240-242), the trajectory log
+//     and the controller's delay prediction delay_buffer_sim (NMPC_controller.m:112-120) into the
+//     solver's x0;
+//   plant_kernel: the controller input buffer push (helper.m:255), the plant x(:,i+1) = x(:,i) +
+//     Ts * evalModelVariableShape(x(:,i), u) with the plant's own delay buffer (:289-307), logs.
+
+// |C(s) - p|^2 with C at the floor-mod of s (evalSpline, bspline_shape.m:192-199)
+__device__ __forceinline__ double contact_phi(const ShapeDev& sh, double s, double px, double py) {
+    SplineEval e;
+    spline_eval(sh, mat_mod(s, sh.b), e);
+    const double ex = e.C[0] - px, ey = e.C[1] - py;
+    return ex * ex + ey * ey;
 }
 
-__global__ void plant_kernel(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
-                             const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
-                             double* Xtraj, double* Utraj, int32_t* Straj) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
+// The contact point after a lateral disturbance: argmin_s |C(s) - p|^2 from s0 (fminunc in the
+// reference, helper.m:230; restated as a damped Newton iteration, as the oracle's reproject_contact)
+__device__ double reproject_contact(const ShapeDev& sh, double px, double py, double s0) {
+    double s = s0, phi = contact_phi(sh, s, px, py);
+    for (int it = 0; it < 60; ++it) {
+        SplineEval e;
+        spline_eval(sh, mat_mod(s, sh.b), e);
+        const double ex = e.C[0] - px, ey = e.C[1] - py;
+        const double g = 2.0 * (ex * e.D[0] + ey * e.D[1]);
+        const double h = 2.0 * (e.D[0] * e.D[0] + e.D[1] * e.D[1] + ex * e.Dd[0] + ey * e.Dd[1]);
+        if (fabs(g) < 1e-14) break;
+        double step = h > 0.0 ? -g / h : (g > 0.0 ? -0.05 : 0.05) * sh.b;
+        const double smax = 0.25 * sh.b;
+        step = fmin(fmax(step, -smax), smax);
+        bool ok = false;
+        double sn = s, phin = phi;
+        for (int k = 0; k < 60; ++k) {
+            sn = s + step;
+            phin = contact_phi(sh, sn, px, py);
+            if (phin < phi) { ok = true; break; }
+            step *= 0.5;
+        }
+        if (!ok) break;
+        s = sn;
+        phi = phin;
+        if (fabs(step) < 1e-13 * sh.b) break;
+    }
+    return s;
+}
+
+__device__ __forceinline__ const ShapeDev& shape_clamped(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int i) {
     const int id = sid ? sid[i] : 0;   // clamped like shape_of (the table may have shrunk since the ids were set)
-    const ShapeDev& sh = shapes[id < 0 ? 0 : (id >= n_shapes ? n_shapes - 1 : id)];
-    double xi[4] = {x[(size_t)i * 4], x[(size_t)i * 4 + 1], x[(size_t)i * 4 + 2], x[(size_t)i * 4 + 3]};
-    const double u[2] = {u0[(size_t)i * 2], u0[(size_t)i * 2 + 1]};
-    DynOut d;
-    dynamics<false>(sh, xi[2], xi[3], u[0], u[1], d);
-    for (int c = 0; c < 4; ++c) {
-        double v = xi[c] + Ts * d.f[c];
-        if (noise_next) v += noise_next[(size_t)i * 4 + c];
-        x[(size_t)i * 4 + c] = v;
-        Xtraj[((size_t)i * (n_steps + 1) + step + 1) * 4 + c] = v;
-    }
-    Utraj[((size_t)i * n_steps + step) * 2] = u[0];
-    Utraj[((size_t)i * n_steps + step) * 2 + 1] = u[1];
-    if (Straj) Straj[(size_t)i * n_steps + step] = status[i];
+    return shapes[id < 0 ? 0 : (id >= n_shapes ? n_shapes - 1 : id)];
 }
 
-hipError_t launch_closed_loop_init(int B, double* x, const double* noise0, double* Xtraj, int n_steps,
-                                   hipStream_t stream) {
-    hipLaunchKernelGGL(closed_loop_init_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, B, x, noise0, Xtraj,
-                       n_steps);
+__global__ void closed_loop_pre_kernel(ClosedLoopArgs a, int t) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.B) return;
+    const ShapeDev& sh = shape_clamped(a.shapes, a.n_shapes, a.sid, i);
+    double x[4] = {a.x[(size_t)i * 4], a.x[(size_t)i * 4 + 1], a.x[(size_t)i * 4 + 2], a.x[(size_t)i * 4 + 3]};
+    if (a.dist_step > 0 && t + 1 == a.dist_step) {
+        // y += amplitude; new contact: the spline point nearest (-xwidth/2, C_y(s) - amplitude),
+        // from s0_spline = 0 (one disturbance per run), wrapped into [-b, b) (:224-234)
+        const double amp = a.dist_amp ? a.dist_amp[i] : 0.0;
+        x[1] += amp;
+        SplineEval e;
+        spline_eval(sh, mat_mod(x[3], sh.b), e);
+        const double sn = reproject_contact(sh, -0.5 * sh.xwidth, e.C[1] - amp, 0.0);
+        x[3] = mat_mod(sn, sh.b) - sh.b * (sn < 0.0 ? 1.0 : 0.0);
+    }
+    if (a.noise)
+        for (int c = 0; c < 4; ++c) x[c] += a.noise[((size_t)t * a.B + i) * 4 + c];
+    for (int c = 0; c < 4; ++c) {
+        a.x[(size_t)i * 4 + c] = x[c];
+        a.Xtraj[((size_t)i * (a.n_steps + 1) + t) * 4 + c] = x[c];
+    }
+    // delay_buffer_sim: D Euler steps with the buffered inputs, oldest (u_buff_contr(:, end)) first
+    for (int k = 1; k <= a.D; ++k) {
+        const double* u = a.ubc + ((size_t)i * a.D + (a.D - k)) * 2;
+        DynOut d;
+        dynamics<false>(sh, x[2], x[3], u[0], u[1], d);
+        for (int c = 0; c < 4; ++c) x[c] += a.Ts * d.f[c];
+    }
+    for (int c = 0; c < 4; ++c) a.xs[(size_t)i * 4 + c] = x[c];
+    if (a.Xsim)
+        for (int c = 0; c < 4; ++c) a.Xsim[((size_t)i * a.n_steps + t) * 4 + c] = x[c];
+}
+
+__global__ void plant_kernel(ClosedLoopArgs a, int t) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.B) return;
+    const ShapeDev& sh = shape_clamped(a.shapes, a.n_shapes, a.sid, i);
+    double xi[4] = {a.x[(size_t)i * 4], a.x[(size_t)i * 4 + 1], a.x[(size_t)i * 4 + 2], a.x[(size_t)i * 4 + 3]};
+    const double u[2] = {a.u0[(size_t)i * 2], a.u0[(size_t)i * 2 + 1]};
+    // u_buff_contr = [u, u_buff_contr(:, 1:end-1)]
+    if (a.D > 0) {
+        double* b = a.ubc + (size_t)i * a.D * 2;
+        for (int k = a.D - 1; k >= 1; --k) { b[2 * k] = b[2 * (k - 1)]; b[2 * k + 1] = b[2 * (k - 1) + 1]; }
+        b[0] = u[0];
+        b[1] = u[1];
+    }
+    double ua[2] = {u[0], u[1]};
+    if (a.Dp > 0) {   // the plant applies u_buff_plant(:, end), then pushes u
+        double* b = a.ubp + (size_t)i * a.Dp * 2;
+        ua[0] = b[2 * (a.Dp - 1)];
+        ua[1] = b[2 * (a.Dp - 1) + 1];
+        for (int k = a.Dp - 1; k >= 1; --k) { b[2 * k] = b[2 * (k - 1)]; b[2 * k + 1] = b[2 * (k - 1) + 1]; }
+        b[0] = u[0];
+        b[1] = u[1];
+    }
+    DynOut d;
+    dynamics<false>(sh, xi[2], xi[3], ua[0], ua[1], d);
+    for (int c = 0; c < 4; ++c) {
+        const double v = xi[c] + a.Ts * d.f[c];
+        a.x[(size_t)i * 4 + c] = v;
+        if (t + 1 == a.n_steps) a.Xtraj[((size_t)i * (a.n_steps + 1) + t + 1) * 4 + c] = v;
+    }
+    a.Utraj[((size_t)i * a.n_steps + t) * 2] = u[0];
+    a.Utraj[((size_t)i * a.n_steps + t) * 2 + 1] = u[1];
+    if (a.Straj) a.Straj[(size_t)i * a.n_steps + t] = a.status[i];
+}
+
+// NMPC_controller.delay_buffer_sim alone (qsp_delay_buffer_sim)
+__global__ void delay_sim_kernel(ClosedLoopArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.B) return;
+    const ShapeDev& sh = shape_clamped(a.shapes, a.n_shapes, a.sid, i);
+    double x[4] = {a.x[(size_t)i * 4], a.x[(size_t)i * 4 + 1], a.x[(size_t)i * 4 + 2], a.x[(size_t)i * 4 + 3]};
+    for (int k = 1; k <= a.D; ++k) {
+        const double* u = a.ubc + ((size_t)i * a.D + (a.D - k)) * 2;
+        DynOut d;
+        dynamics<false>(sh, x[2], x[3], u[0], u[1], d);
+        for (int c = 0; c < 4; ++c) x[c] += a.Ts * d.f[c];
+    }
+    for (int c = 0; c < 4; ++c) a.xs[(size_t)i * 4 + c] = x[c];
+}
+
+__global__ void reproject_kernel(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int n, const double* px,
+                                 const double* py, const double* s0, double* s) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    s[i] = reproject_contact(shape_clamped(shapes, n_shapes, sid, i), px[i], py[i], s0[i]);
+}
+
+hipError_t launch_closed_loop_pre(const ClosedLoopArgs& a, int t, hipStream_t stream) {
+    hipLaunchKernelGGL(closed_loop_pre_kernel, dim3((a.B + 127) / 128), dim3(128), 0, stream, a, t);
     return hipGetLastError();
 }
 
-hipError_t launch_plant(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int B, double Ts, double* x,
-                        const double* u0, const int32_t* status, int step, int n_steps, const double* noise_next,
-                        double* Xtraj, double* Utraj, int32_t* Straj, hipStream_t stream) {
-    hipLaunchKernelGGL(plant_kernel, dim3((B + 127) / 128), dim3(128), 0, stream, shapes, n_shapes, sid, B, Ts, x, u0,
-                       status, step, n_steps, noise_next, Xtraj, Utraj, Straj);
+hipError_t launch_plant(const ClosedLoopArgs& a, int t, hipStream_t stream) {
+    hipLaunchKernelGGL(plant_kernel, dim3((a.B + 127) / 128), dim3(128), 0, stream, a, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_delay_sim(const ClosedLoopArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(delay_sim_kernel, dim3((a.B + 127) / 128), dim3(128), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reproject(const ShapeDev* shapes, int n_shapes, const int32_t* sid, int n, const double* px,
+                            const double* py, const double* s0, double* s, hipStream_t stream) {
+    hipLaunchKernelGGL(reproject_kernel, dim3((n + 127) / 128), dim3(128), 0, stream, shapes, n_shapes, sid, n, px, py,
+                       s0, s);
     return hipGetLastError();
 }
 

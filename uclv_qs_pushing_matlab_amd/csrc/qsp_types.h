@@ -15,6 +15,7 @@ struct ShapeDev {
     double c;                              // c_ellipse = tau_max / (mu_sg m g)
     double mu;                             // mu_sp
     double inv_h;                          // 1 / interior knot spacing (span guess only)
+    double xwidth;                         // slider width along x (object_selection.m; disturbance re-projection)
     double knots[QSP_MAX_CTRL + 4];        // S, n + 4 entries
     double ctrl[2 * QSP_MAX_CTRL];         // P_i (x, y)
     double dctrl[2 * QSP_MAX_CTRL];        // cd_i = 3 (P_i - P_{i-1}) / (S_{i+3} - S_i), cd_0 = 0

@@ -47,4 +47,5 @@ def make_shape(name, slider=None, pcl_path=None):
     rc = _lib.lib().qsp_shape_from_ply(path.encode(), _FLIP.get(name, 0), slider["mu_sg"], slider["mu_sp"],
                                        slider["m"], slider["tau_max"], sh)
     _lib.check(rc, "qsp_shape_from_ply")
+    sh.xwidth = slider["xwidth"]          # contact re-projection after a disturbance (helper.m:229)
     return sh

@@ -262,19 +262,59 @@ class OcpSolver:
         self._timed(lambda: check(self._L.qsp_controller_solve(self._h, ptr(x0), ptr(idx)), "qsp_controller_solve"))
         return self.get_u0()
 
-    def closed_loop(self, x0, n_steps, index0=1, noise=None):
-        """Device-resident closed loop (helper.m:195-322): returns X (B, n+1, 4), U (B, n, 2),
-        status (B, n).  noise: (n, B, 4) additive state noise before each solve, or None."""
+    def closed_loop(self, x0, n_steps, index0=1, noise=None, plant_delay=0.0, disturbance=False, t_dist=0,
+                    amplitude=None):
+        """Device-resident closed loop (helper.m:195-322): returns X (B, n+1, 4) (plant states after
+        disturbance and noise), Xsim (B, n, 4) (the delay-predicted states the solver sees), U (B, n, 2),
+        status (B, n).  noise: (n, B, 4) additive state noise before each solve, or None; plant_delay [s];
+        disturbance at the 1-based step t_dist with per-lane amplitude (y offset + contact re-projection)."""
         n = int(n_steps)
         x0 = f64(self._lanes(x0, 4))
         idx = i32(np.broadcast_to(np.asarray(index0, np.int32), (self.B,)))
         nz = None if noise is None else f64(noise, (n, self.B, 4))
+        amp = None if amplitude is None else f64(np.broadcast_to(np.asarray(amplitude, np.float64), (self.B,)))
+        o = _lib.ClosedLoopOpts()
+        o.plant_delay, o.disturbance, o.t_dist = float(plant_delay), 1 if disturbance else 0, int(t_dist)
+        o.amplitude = None if amp is None else amp.ctypes.data
         X = np.zeros((self.B, n + 1, 4))
+        Xs = np.zeros((self.B, n, 4))
         U = np.zeros((self.B, n, 2))
         st = np.zeros((self.B, n), np.int32)
-        check(self._L.qsp_closed_loop(self._h, ptr(x0), ptr(idx), n, ptr(nz), ptr(X), ptr(U), ptr(st)),
-              "qsp_closed_loop")
-        return dict(X=X, U=U, status=st)
+        check(self._L.qsp_closed_loop_ex(self._h, C.byref(o), ptr(x0), ptr(idx), n, ptr(nz), ptr(X), ptr(Xs), ptr(U),
+                                         ptr(st)), "qsp_closed_loop_ex")
+        return dict(X=X, Xsim=Xs, U=U, status=st)
+
+    # ------------------------------------------------ delay compensation
+    def set_delay_comp(self, delay):
+        """set_delay_comp (NMPC_controller.m:106-110): delay_buff_comp = ceil(delay / Ts)."""
+        check(self._L.qsp_set_delay_comp(self._h, float(delay)), "qsp_set_delay_comp")
+
+    def delay_cols(self):
+        d = C.c_int32()
+        check(self._L.qsp_get_delay_comp(self._h, C.byref(d)), "qsp_get_delay_comp")
+        return d.value
+
+    def delay_buffer_sim(self, x):
+        """delay_buffer_sim (NMPC_controller.m:112-120) on the device, per lane."""
+        x = f64(self._lanes(x, 4))
+        out = np.zeros((self.B, 4))
+        check(self._L.qsp_delay_buffer_sim(self._h, ptr(x), ptr(out)), "qsp_delay_buffer_sim")
+        return out
+
+    def delay_buffer_push(self, u):
+        """u_buff_contr = [u, u_buff_contr(:, 1:end-1)] (helper.m:255)."""
+        u = f64(self._lanes(u, 2))
+        check(self._L.qsp_delay_buffer_push(self._h, ptr(u)), "qsp_delay_buffer_push")
+
+    def reproject_contact(self, px, py, s0, shape_id=None):
+        px = f64(px).ravel()
+        n = len(px)
+        py = f64(np.broadcast_to(py, (n,)))
+        s0 = f64(np.broadcast_to(s0, (n,)))
+        out = np.zeros(n)
+        check(self._L.qsp_reproject_contact(self._h, n, ptr(self._sid(shape_id, n)), ptr(px), ptr(py), ptr(s0),
+                                            ptr(out)), "qsp_reproject_contact")
+        return out
 
     def controller_reset(self):
         check(self._L.qsp_controller_reset(self._h), "qsp_controller_reset")
