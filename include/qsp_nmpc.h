@@ -162,6 +162,21 @@ int qsp_get_qp_iter(qsp_solver* s, int32_t* qp_iter /* B, summed over the SQP it
  * test (their last iterate is used, as HPIPM's at iter_max): B counts */
 int qsp_get_qp_capped(qsp_solver* s, int32_t* capped /* B */);
 int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
+/* dims of the handle (outputs of a MEX/FFI layer are sized from these, never from caller input) */
+int qsp_get_dims(const qsp_solver* s, int32_t* N, int32_t* B);
+/* the acados field-by-field setters: set('cost_y_ref', y, k) for one stage k in 0..N-1 (B x 6),
+ * set('cost_y_ref_e', y_e, N) (B x 4), set('init_x'/'init_u'/'init_pi') one at a time */
+int qsp_set_yref_stage(qsp_solver* s, int32_t stage, const double* y /* B x 6 */);
+int qsp_set_yref_e(qsp_solver* s, const double* y_e /* B x 4 */);
+int qsp_set_init_x(qsp_solver* s, const double* X /* B x (N+1) x 4 */);
+int qsp_set_init_u(qsp_solver* s, const double* U /* B x N x 2 */);
+int qsp_set_init_pi(qsp_solver* s, const double* PI /* B x N x 4 */);
+/* acados get('time_tot'/'time_lin'/'time_qp_sol') in seconds (helper.m:264-269): with qsp_set_timing(s, 1)
+ * every solve records HIP events at its kernel boundaries and qsp_get_timings reports the last solve
+ * (time_lin = the separate linearisation / packing-sort kernels, time_qp_sol = the QP kernels, which in
+ * nlp_mode 0 include the fused linearisation); without it time_lin / time_qp_sol are NaN. */
+int qsp_set_timing(qsp_solver* s, int32_t on);
+int qsp_get_timings(qsp_solver* s, double* time_tot, double* time_lin, double* time_qp_sol);
 
 /* --------------------------------------- NMPC_controller.solve(x0, index_time) */
 /* reference table y_ref (6 x T, MATLAB column-major == T x 6 row-major), shared by all lanes

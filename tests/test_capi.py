@@ -109,9 +109,13 @@ def test_product_does_not_import_oracle():
                 assert not pat.search(open(os.path.join(dirpath, f)).read()), f
 
 
-def test_mex_gateway_compiles():
-    """integration/matlab/qsp_nmpc_mex.c type-checks against the C ABI (MEX API from a
-    declaration-only stub; MATLAB is absent)."""
-    src = os.path.join(ROOT, "integration", "matlab", "qsp_nmpc_mex.c")
-    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
-                           "-I", os.path.join(ROOT, "tests", "stubs"), src])
+def test_mex_gateway_compiles(tmp_path):
+    """integration/matlab/qsp_nmpc_mex.c compiles and links unmodified with the functional MEX
+    stand-in and the driver (run on the GPU: tests/test_gpu_mex.py)."""
+    lib = os.path.join(ROOT, "uclv_qs_pushing_matlab_amd")
+    subprocess.check_call(["gcc", "-std=c99", "-D_DEFAULT_SOURCE", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "tests", "stubs"),
+                           os.path.join(ROOT, "integration", "matlab", "qsp_nmpc_mex.c"),
+                           os.path.join(ROOT, "tests", "stubs", "mex_stub.c"),
+                           os.path.join(ROOT, "tests", "stubs", "mex_driver.c"),
+                           "-L", lib, "-lqsp_nmpc", "-lm", "-o", str(tmp_path / "mex_driver")])

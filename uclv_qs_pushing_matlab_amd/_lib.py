@@ -86,6 +86,14 @@ _SIGS = {
     "qsp_get_qp_iter": [_P, _P],
     "qsp_get_qp_capped": [_P, _P],
     "qsp_get_time_tot": [_P, C.POINTER(_D)],
+    "qsp_get_dims": [_P, C.POINTER(_I), C.POINTER(_I)],
+    "qsp_set_yref_stage": [_P, _I, _P],
+    "qsp_set_yref_e": [_P, _P],
+    "qsp_set_init_x": [_P, _P],
+    "qsp_set_init_u": [_P, _P],
+    "qsp_set_init_pi": [_P, _P],
+    "qsp_set_timing": [_P, _I],
+    "qsp_get_timings": [_P, C.POINTER(_D), C.POINTER(_D), C.POINTER(_D)],
     "qsp_set_reference_trajectory": [_P, _P, _I],
     "qsp_set_reference_trajectories": [_P, _P, _I],
     "qsp_gen_straight_lines": [_P, _P, _P, _D, _D, _I, C.POINTER(_I)],

@@ -72,6 +72,7 @@ struct qsp_solver {
     int kev_used = 0;
     std::vector<int> kev_solves;   // event offset of each timed solve
     std::vector<int> kev_split;    // ... and whether its SQP loop ran in two parts
+    bool auto_timing = false;      // qsp_set_timing: every solve times its kernels (acados time_lin / time_qp_sol)
     // two-stream SQP loop (launch_sqp): second stream, fork/join events, requested parts (0 = auto)
     SqpStreams split;
     int parts_req = 0;
@@ -93,9 +94,15 @@ static const SqpStreams* sqp_split(qsp_solver* s) {
     return &s->split;
 }
 
-// events for one timed solve (nullptr when timing is off or the pool is used up)
+// events for one timed solve (nullptr when timing is off or the pool is used up); with
+// qsp_set_timing the one-solve pool is reused by every solve (the last one is reported)
 static hipEvent_t* take_kernel_events(qsp_solver* s) {
     const int per = 2 * s->o.sqp_iters + 3;
+    if (s->auto_timing) {
+        s->kev_used = 0;
+        s->kev_solves.clear();
+        s->kev_split.clear();
+    }
     if (s->kev.empty() || s->kev_used + per > (int)s->kev.size()) return nullptr;
     s->kev_solves.push_back(s->kev_used);
     s->kev_split.push_back((sqp_split(s)->parts > 1 || s->split.fused) ? 1 : 0);
@@ -103,6 +110,8 @@ static hipEvent_t* take_kernel_events(qsp_solver* s) {
     s->kev_used += per;
     return e;
 }
+
+static int kernel_times_of(qsp_solver* s, double* ms, int32_t* launches);
 
 static void fill_params(qsp_solver* s) {
     SolveParams& p = s->p;
@@ -668,6 +677,68 @@ int qsp_get_time_tot(qsp_solver* s, double* ms) {
     return QSP_OK;
 }
 
+int qsp_get_dims(const qsp_solver* s, int32_t* N, int32_t* B) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_get_dims: null handle");
+    if (N) *N = s->o.N;
+    if (B) *B = s->o.batch;
+    return QSP_OK;
+}
+
+int qsp_set_yref_stage(qsp_solver* s, int32_t k, const double* y) {
+    if (!s || !y) return fail(QSP_ERR_ARG, "qsp_set_yref_stage: null argument");
+    if (k < 0 || k >= s->o.N) return fail(QSP_ERR_ARG, "qsp_set_yref_stage: stage out of range 0..N-1");
+    HIPCHK(hipSetDevice(s->o.device));
+    // column k of every lane's N x 6 block: a strided copy (B rows of 6 doubles)
+    HIPCHK(hipMemcpy2DAsync(s->yref.as<double>() + (size_t)k * 6, (size_t)s->o.N * 6 * 8, y, 6 * 8, 6 * 8,
+                            (size_t)s->o.batch, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return QSP_OK;
+}
+
+int qsp_set_yref_e(qsp_solver* s, const double* y_e) {
+    if (!s || !y_e) return fail(QSP_ERR_ARG, "qsp_set_yref_e: null argument");
+    return h2d(s, s->yref_e, y_e, (size_t)s->o.batch * 4 * 8);
+}
+
+int qsp_set_init_x(qsp_solver* s, const double* X) {
+    if (!s || !X) return fail(QSP_ERR_ARG, "qsp_set_init_x: null argument");
+    return h2d(s, s->X, X, (size_t)s->o.batch * (s->o.N + 1) * 4 * 8);
+}
+int qsp_set_init_u(qsp_solver* s, const double* U) {
+    if (!s || !U) return fail(QSP_ERR_ARG, "qsp_set_init_u: null argument");
+    return h2d(s, s->U, U, (size_t)s->o.batch * s->o.N * 2 * 8);
+}
+int qsp_set_init_pi(qsp_solver* s, const double* PI) {
+    if (!s || !PI) return fail(QSP_ERR_ARG, "qsp_set_init_pi: null argument");
+    return h2d(s, s->PI, PI, (size_t)s->o.batch * s->o.N * 4 * 8);
+}
+
+int qsp_set_timing(qsp_solver* s, int32_t on) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_set_timing: null handle");
+    int r = qsp_set_kernel_timing(s, on ? 1 : 0);
+    if (r) return r;
+    s->auto_timing = on != 0;
+    return QSP_OK;
+}
+
+int qsp_get_timings(qsp_solver* s, double* time_tot, double* time_lin, double* time_qp_sol) {
+    if (!s) return fail(QSP_ERR_ARG, "qsp_get_timings: null handle");
+    if (time_tot) *time_tot = s->last_ms * 1e-3;
+    double lin = NAN, qp = NAN;
+    if (s->auto_timing && !s->kev_solves.empty()) {
+        double ms[4];
+        int32_t n[4];
+        HIPCHK(hipSetDevice(s->o.device));
+        const int r = kernel_times_of(s, ms, n);   // the last solve's events stay readable
+        if (r) return r;
+        lin = ms[1] * 1e-3;
+        qp = ms[2] * 1e-3;
+    }
+    if (time_lin) *time_lin = lin;
+    if (time_qp_sol) *time_qp_sol = qp;
+    return QSP_OK;
+}
+
 // ------------------------------------------------------ controller level
 int qsp_set_reference_trajectory(qsp_solver* s, const double* traj, int32_t T) {
     if (!s || !traj || T < 1) return fail(QSP_ERR_ARG, "qsp_set_reference_trajectory: bad argument");
@@ -973,9 +1044,8 @@ int qsp_set_kernel_timing(qsp_solver* s, int32_t max_solves) {
     return QSP_OK;
 }
 
-int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
-    if (!s || !ms || !launches) return fail(QSP_ERR_ARG, "qsp_get_kernel_times: null argument");
-    HIPCHK(hipSetDevice(s->o.device));
+// summed kernel times of the recorded solves (events kept: the pool is re-armed by the caller)
+static int kernel_times_of(qsp_solver* s, double* ms, int32_t* launches) {
     for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; }
     const int K = s->o.sqp_iters;
     for (size_t j = 0; j < s->kev_solves.size(); ++j) {
@@ -993,6 +1063,14 @@ int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
         }
         HIPCHK(hipEventElapsedTime(&t, e[2 * K + 1], e[2 * K + 2])); ms[3] += t; launches[3] += 1;
     }
+    return QSP_OK;
+}
+
+int qsp_get_kernel_times(qsp_solver* s, double* ms, int32_t* launches) {
+    if (!s || !ms || !launches) return fail(QSP_ERR_ARG, "qsp_get_kernel_times: null argument");
+    HIPCHK(hipSetDevice(s->o.device));
+    const int r = kernel_times_of(s, ms, launches);
+    if (r) return r;
     s->kev_solves.clear();
     s->kev_split.clear();
     s->kev_used = 0;
