@@ -67,6 +67,27 @@ CONFIG3_BATCH = 262144         # BASELINE configs[3]: sharded over the GPUs of o
 SEED = 20250303 + 3
 
 
+def config4_inputs(B, N, seed, lo=0, hi=None):
+    """BASELINE configs[4]: N = 50, the curved x_finals.mat reference (x, y, theta; s_ref = 0) with a
+    random start index per lane in [1, 797 - N], x0 near the reference start (s inside its bounds),
+    shapes mixed per lane; per-lane y_ref staged on the host (lanes [lo, hi) of a B-lane job)."""
+    from uclv_qs_pushing_matlab_amd.objects import DATA_DIR
+    hi = B if hi is None else hi
+    xf = np.load(os.path.join(DATA_DIR, "x_finals.npz"))
+    traj = np.zeros((len(xf["x"]), 6))
+    traj[:, 0], traj[:, 1], traj[:, 2] = xf["x"], xf["y"], xf["theta"]
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(1, len(traj) - N, B).astype(np.int32)
+    x0 = traj[idx - 1, :4] + np.stack([rng.uniform(-0.005, 0.005, B), rng.uniform(-0.005, 0.005, B),
+                                       rng.uniform(-0.05, 0.05, B), rng.uniform(-0.03, 0.005, B)], 1)
+    idx, x0 = idx[lo:hi], x0[lo:hi]
+    cols = np.minimum(idx[:, None] + np.arange(N)[None, :], len(traj)) - 1          # get_y_ref clamp
+    yref = traj[cols]
+    yref_e = yref[:, N - 1, :4].copy()
+    shape_id = (np.arange(lo, hi) % len(SHAPES)).astype(np.int32)
+    return x0, yref, yref_e, shape_id, traj, idx
+
+
 def config1_inputs(N, B=4096, seed=20250303 + 1):
     """BASELINE configs[1]: B = 4 096 random x0 (config-2 law) around santal, straight x_ref."""
     x0 = config2_x0(B, seed)
@@ -164,8 +185,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--global-batch", type=int, default=0,
-                    help="lanes over all GPUs (0: 65 536 = configs[2] on one GPU, 262 144 = configs[3] on several)")
-    ap.add_argument("--N", type=int, default=20)
+                    help="lanes over all GPUs (0: the configuration's batch: 65 536 = configs[2] on one GPU, "
+                         "262 144 = configs[3] on several, 16 384 for configs[4])")
+    ap.add_argument("--config", type=int, default=0, choices=(0, 2, 4),
+                    help="BASELINE configuration: 0 = the metric's (configs[2] on one GPU, configs[3] on several); "
+                         "4 = N = 50 over the curved x_finals reference")
+    ap.add_argument("--N", type=int, default=0, help="horizon (0: the configuration's, 20 or 50)")
     ap.add_argument("--sqp-iters", type=int, default=50)
     ap.add_argument("--qp-iters", type=int, default=20)
     ap.add_argument("--stages-per-lane", type=int, default=0)
@@ -202,10 +227,15 @@ def main():
     from uclv_qs_pushing_matlab_amd.objects import make_shape
     from uclv_qs_pushing_matlab_amd.solver import OcpSolver
 
-    N, K = args.N, args.sqp_iters
-    total = args.global_batch or (CONFIG2_BATCH if world == 1 else CONFIG3_BATCH)
+    cfg4 = args.config == 4
+    N, K = args.N or (50 if cfg4 else 20), args.sqp_iters
+    total = args.global_batch or (16384 if cfg4 else (CONFIG2_BATCH if world == 1 else CONFIG3_BATCH))
     lo, hi = shard_range(total, world, rank)        # this rank's shard of the global lane set
-    x0, yref, yref_e, sid, traj = make_inputs(total, N, args.seed, lo, hi)
+    if cfg4:
+        x0, yref, yref_e, sid, traj, idx4 = config4_inputs(total, N, args.seed, lo, hi)
+    else:
+        x0, yref, yref_e, sid, traj = make_inputs(total, N, args.seed, lo, hi)
+        idx4 = None
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
@@ -307,7 +337,10 @@ def main():
     value = total_solves / elapsed
     avg_kern_s = float(np.mean(kern_ms)) * 1e-3
     achieved = qp_flops_launch / qp_avg_s / 1e12
-    if world == 1:
+    if cfg4:
+        workload = (f"BASELINE configs[4]: batch={total} over {world} GPU(s), curved x_finals reference, "
+                    "random start index per lane")
+    elif world == 1:
         workload = f"BASELINE configs[2]: batch={total} on 1 GPU"
     else:
         workload = (f"BASELINE configs[3]: global batch={total} sharded over {world} GPUs "
@@ -357,17 +390,18 @@ def main():
         # host memory and u0 copied back, y_ref staged on the device from the shared table
         solver.set_shape_ids(sid)
         solver.set_reference_trajectory(traj)
-        solver.controller_solve(x0, 1)
+        idx_h = idx4 if cfg4 else 1
+        solver.controller_solve(x0, idx_h)
         solver.controller_reset()
         th = time.perf_counter()
         nrep = max(1, min(args.steps, 3))
         for _ in range(nrep):
             solver.controller_reset()
-            solver.controller_solve(x0, 1)
+            solver.controller_solve(x0, idx_h)
         result["host_boundary_solves_per_s"] = Bl * nrep / (time.perf_counter() - th)
     solver.close()
 
-    if rank == 0 and world == 1 and not args.no_configs1:
+    if rank == 0 and world == 1 and not args.no_configs1 and not cfg4:
         # BASELINE configs[1] beside the headline (its own GPU timing; CPU in full below)
         x1, traj1, sid1 = config1_inputs(N)
         s1 = OcpSolver(N=N, batch=len(x1), sqp_iters=K, qp_iters=args.qp_iters, device=gpu, nlp_solver_type=args.nlp)
@@ -386,7 +420,7 @@ def main():
         u1_gpu = s1.get_u0()
         s1.close()
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not cfg4:
         hc = host_cpu()
         threads = hc["threads"]
         n, dt, r, run = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, 1 if args.nlp == "SQP" else 0)
