@@ -480,14 +480,18 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         if (fabs(qp->dx0[i]) > rb0) rb0 = fabs(qp->dx0[i]);
     }
 
+    double rs_stop = o->res_stop / r0;
+    if (o->qp_tol_stat / rg0 < rs_stop) rs_stop = o->qp_tol_stat / rg0;
+    if (o->qp_tol_eq / rb0 < rs_stop) rs_stop = o->qp_tol_eq / rb0;
     int nit = 0, converged = 0, stall = 0;
     for (int it = 0; it <= o->qp_iters && !infeasible; ++it) {
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
         mu /= (double)m;
-        /* HPIPM's four exit residuals: complementarity, bound, stationarity, equality */
-        if (!(mu >= o->mu_stop) && !(r0 * rscale >= o->res_stop) && !(rg0 * rscale >= o->qp_tol_stat) &&
-            !(rb0 * rscale >= o->qp_tol_eq)) { converged = 1; break; }
+        /* HPIPM's four exit residuals: complementarity, and the bound, stationarity and equality
+         * residuals r0, rg0, rb0 times their common scale prod(1 - alpha) -- tested as
+         * prod < min(tol / r) (x / 0 = inf: a residual that starts at zero never binds) */
+        if (!(mu >= o->mu_stop) && !(rscale >= rs_stop)) { converged = 1; break; }
         if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
         if (o->qp_stall_iters > 0 && stall >= o->qp_stall_iters) break;   /* stalled: as at the cap */
         nit++;

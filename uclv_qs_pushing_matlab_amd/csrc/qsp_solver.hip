@@ -688,7 +688,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 // residuals are those of the IPM iterate (z, pi, lam, t) with start z = 0, pi = 0, lam =
 // mu0 / t: every Newton step solves them exactly and the update scales all of them by
 // (1 - alpha), so each is its start value times prod(1 - alpha) (tracked, not recomputed:
-// r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)).
+// r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)); the
+// test r * prod < tol is applied as prod < min(tol / r) over the three.
 template <int S>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool& conv,
                       bool skip = false) {
@@ -734,9 +735,12 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
             st.f(F_VN, ls, q) = 0.0;
         }
     }
-    r0 = group_max(r0, c.gs);
-    rg0 = group_max(rg0, c.gs);
-    rb0 = group_max(rb0, c.gs);
+    // the three linear residuals share the scale prod(1 - alpha): one threshold on it
+    // (x / 0 = inf: a residual that starts at zero never binds)
+    double rs_stop = p.res_stop / group_max(r0, c.gs);
+    const double rs_g = p.qp_tol_stat / group_max(rg0, c.gs), rs_b = p.qp_tol_eq / group_max(rb0, c.gs);
+    rs_stop = rs_g < rs_stop ? rs_g : rs_stop;   // (as the oracle: a NaN start residual keeps NaN)
+    rs_stop = rs_b < rs_stop ? rs_b : rs_stop;
     double rscale = 1.0;
     int nit = 0, stall = 0;
     for (int it = 0;; ++it) {
@@ -746,8 +750,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
             for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
         const double mu = group_sum(tl_sum, c.gs) / m;
-        conv = skip || (!(mu >= p.mu_stop) && !(r0 * rscale >= p.res_stop) && !(rg0 * rscale >= p.qp_tol_stat) &&
-                        !(rb0 * rscale >= p.qp_tol_eq));
+        conv = skip || (!(mu >= p.mu_stop) && !(rscale >= rs_stop));
         // stall exit (locally infeasible QP: the step length stays tiny while mu grows): stops
         // like the cap, after the stop test had its chance
         const bool done = conv || (p.qp_stall_iters > 0 && stall >= p.qp_stall_iters);
