@@ -159,6 +159,7 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp):
     out = {"lanes": int(n), "max_abs_u0_err": float(d.max()),
            "nonchaotic_lanes": int(nonchaotic.sum()),
            "max_abs_u0_err_nonchaotic": float(d[nonchaotic].max()) if nonchaotic.any() else None,
+           "frac_nonchaotic_err_le_1e-6": float(np.mean(d[nonchaotic] <= 1e-6)) if nonchaotic.any() else None,
            "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
            "oracle_self_frac_le_1e-6": float(np.mean(self_dev <= 1e-6)),
            "chaotic_frac": float(np.mean(self_dev > 1e-6)),
