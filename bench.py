@@ -200,6 +200,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] (B = 4 096) side measurement")
+    ap.add_argument("--no-configs4", action="store_true", help="skip the configs[4] (N = 50, B = 16 384) side measurement")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
                     help="SQP_RTI: fixed-K full steps (the BASELINE metric); SQP: the reference's merit-backtracking "
                          "SQP with KKT tolerances (sqp_iters = max_iter)")
@@ -421,6 +422,30 @@ def main():
         u1_gpu = s1.get_u0()
         s1.close()
 
+    if rank == 0 and world == 1 and not args.no_configs4 and not cfg4 and args.nlp == "SQP_RTI":
+        # BASELINE configs[4] beside the headline: N = 50, B = 16 384, curved x_finals reference with a
+        # random start index per lane (bench.py --config 4 measures it as the main line)
+        x4, _, _, sid4, traj4, idx4b = config4_inputs(16384, 50, args.seed)
+        s4 = OcpSolver(N=50, batch=len(x4), sqp_iters=K, qp_iters=args.qp_iters, device=gpu)
+        s4.set_shapes([make_shape(n) for n in SHAPES])
+        s4.set_shape_ids(sid4)
+        s4.set_reference_trajectory(traj4)
+        s4.controller_solve(x4, idx4b)
+        s4.synchronize()
+        t4 = time.perf_counter()
+        for _ in range(3):
+            s4.controller_reset()
+            s4.controller_solve(x4, idx4b)
+        s4.synchronize()
+        S4, L4 = s4.layout()
+        result["configs4"] = {"workload": "BASELINE configs[4]: batch=16384, N=50, curved x_finals reference, random "
+                                          "start index per lane, 4 shapes mixed per lane, K=50 SQP-RTI, cold start",
+                              "gpu_solves_per_s": len(x4) * 3 / (time.perf_counter() - t4),
+                              "layout": {"stages_per_lane": S4, "lanes_per_instance": L4},
+                              "note": "host-boundary controller solves (x0 in, u0 out), 3 repeats"}
+        u4_gpu = s4.get_u0()
+        s4.close()
+
     if rank == 0 and world == 1 and not args.no_cpu and not cfg4:
         hc = host_cpu()
         threads = hc["threads"]
@@ -442,6 +467,25 @@ def main():
             result["configs1"].update({"cpu_solves_per_s": len(x1) / dtc, "cpu_seconds": dtc, "cpu_threads": threads,
                                        "cpu_kind": "port (the full batch)",
                                        "frac_lanes_err_le_1e-6": float(np.mean(np.abs(u1_gpu - r1["u0"]).max(1) <= 1e-6))})
+        if "configs4" in result:
+            # configs[4] parity on its first lanes (the probe criterion of parity_leg)
+            from oracle.oracle import Oracle, make_opts
+            orc4 = Oracle(SHAPES)
+            n4 = 64
+
+            def run4(xx, **kw):
+                return orc4.controller_solve(make_opts(N=50, sqp_iters=K, **kw), xx, traj4, idx4b[:n4],
+                                             orc4.new_warm(n4, 50), shape_id=sid4[:n4], nthreads=threads)
+            r4 = run4(x4[:n4])
+            d4 = np.abs(u4_gpu[:n4] - r4["u0"]).max(1)
+            dev4 = np.zeros(n4)
+            for f in (1e-13, -1e-13, 3e-13):
+                dev4 = np.maximum(dev4, np.abs(run4(x4[:n4] * (1 + f))["u0"] - r4["u0"]).max(1))
+            dev4 = np.maximum(dev4, np.abs(run4(x4[:n4], mu_stop=1.5e-10)["u0"] - r4["u0"]).max(1))
+            nc4 = dev4 < 1e-9
+            result["configs4"].update({"parity_lanes": n4, "nonchaotic_lanes": int(nc4.sum()),
+                                       "frac_nonchaotic_err_le_1e-6": float(np.mean(d4[nc4] <= 1e-6)) if nc4.any() else None,
+                                       "frac_lanes_err_le_1e-6": float(np.mean(d4 <= 1e-6))})
     if rank == 0:
         if nbad:
             print(f"bench: WARNING {nbad} of {total} lanes returned a non-zero status", file=sys.stderr)
