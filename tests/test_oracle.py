@@ -236,6 +236,34 @@ def test_vbound_definition(oracle):
     np.testing.assert_allclose(vb, ref, rtol=1e-12)
 
 
+@pytest.mark.parametrize("name", ["santal", "balea", "montana", "pulirapid"])
+def test_tangent_angle_curvature_finite_differences(oracle, name):
+    """The reference's own curvature check (acados_nmpc/t_angle_curvatures.m:1-27): the tangent
+    angle atan2(C'_y, C'_x) on s = 0:1e-3:b, its differences unwrapped where |d| > 3 pi / 2 and
+    divided by ds, against the analytic kappa (d/ds of the angle, bspline_shape.m:137-152) at the
+    interval midpoints, away from the knots (C'' of a cubic spline is only continuous there)."""
+    sid = ["santal", "balea", "montana", "pulirapid"].index(name)
+    b = load_object(name)["b"]
+    h = 1e-3
+    s = np.arange(0.0, b, h)
+    _, dC, _, _, _ = oracle.spline(s, sid)
+    ang = np.arctan2(dC[:, 1], dC[:, 0])
+    d = np.diff(ang)
+    d[np.abs(d) > 1.5 * np.pi] -= 2 * np.pi * np.sign(d[np.abs(d) > 1.5 * np.pi])
+    fd = d / np.diff(s)
+    kap = oracle.spline(s[:-1] + h / 2, sid)[4]
+    # skip the intervals that hold a knot (shapes_np.knots_for: uniform interior spacing)
+    knots = np.unique(load_object(name)["S"])
+    near = np.min(np.abs((s[:-1] + h / 2)[:, None] - knots[None, :]), 1) < h
+    ok = ~near & np.isfinite(kap)
+    scale = np.max(np.abs(kap[ok]))
+    assert ok.sum() > 0.5 * len(ok)
+    # midpoint rule: O(h^2 kappa'') on smooth intervals
+    assert np.median(np.abs(fd[ok] - kap[ok])) < 1e-3 * scale
+    assert np.mean(np.abs(fd[ok] - kap[ok]) < 1e-2 * scale + 1e-6) > 0.97
+    assert np.max(np.abs(fd[ok] - kap[ok])) < 3e-2 * scale
+
+
 def test_decagon_fixture_known_answers():
     """test_bspline_class.m's decagon: clamped-end values, end tangent, convex hull,
     mirror symmetry of the uniform knot vector, C(b) = 0 (half-open indicator)."""
