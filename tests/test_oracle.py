@@ -264,6 +264,45 @@ def test_tangent_angle_curvature_finite_differences(oracle, name):
     assert np.max(np.abs(fd[ok] - kap[ok])) < 3e-2 * scale
 
 
+def _eval_bspline_m(s, S, i, p):
+    """acados_nmpc/eval_bspline.m:1-33 (= bspline_shape.m:40-72) restated literally: 1-based i,
+    the zero-support guard first (also at p = 0), the half-open indicator, the 0/0 guards."""
+    if S[i + p] == S[i - 1]:
+        return 0.0
+    if p == 0:
+        return float(s < S[i]) * float(s >= S[i - 1])
+    a = _eval_bspline_m(s, S, i, p - 1)
+    c = _eval_bspline_m(s, S, i + 1, p - 1)
+    m1 = 0.0 if S[i + p - 1] == S[i - 1] else (s - S[i - 1]) / (S[i + p - 1] - S[i - 1])
+    m2 = 0.0 if S[i + p] == S[i] else (S[i + p] - s) / (S[i + p] - S[i])
+    return m1 * a + m2 * c
+
+
+@pytest.mark.parametrize("name", ["santal", "balea", "montana", "pulirapid"])
+def test_spline_matches_literal_eval_bspline(oracle, name):
+    """The oracle's C(s) and C'(s) against eval_bspline.m's recursion summed as getSymbolicSpline
+    (bspline_shape.m:74-83) and getSymboliSplineDot (:85-104) do, at sampled points, at every
+    knot (the half-open indicator's side) and at s = b (every basis function zero)."""
+    sid = ["santal", "balea", "montana", "pulirapid"].index(name)
+    o = load_object(name)
+    S, P, b, p = list(o["S"]), o["P"], o["b"], 3
+    n = len(P)
+    s = np.r_[np.random.default_rng(7).uniform(0.0, b, 24), np.unique(S)]
+    C, _, D, _, _ = oracle.spline(s, sid)
+    for q, sq in enumerate(s):
+        Cm = np.zeros(2)
+        for i in range(1, n + 1):
+            Cm = Cm + _eval_bspline_m(sq, S, i, p) * P[i - 1]
+        Dm = np.zeros(2)
+        for i in range(2, n + 1):
+            cj = 0.0 if S[i + p - 1] == S[i - 1] else p * (P[i - 1] - P[i - 2]) / (S[i + p - 1] - S[i - 1])
+            Dm = Dm + cj * _eval_bspline_m(sq, S, i, p - 1)
+        np.testing.assert_array_equal(C[q], Cm)                        # same sum, same order: bit for bit
+        np.testing.assert_allclose(D[q], Dm, rtol=0, atol=2e-15)        # the oracle divides the knot span once
+        if sq == b:
+            assert np.all(Cm == 0.0) and np.all(C[q] == 0.0)
+
+
 def test_decagon_fixture_known_answers():
     """test_bspline_class.m's decagon: clamped-end values, end tangent, convex hull,
     mirror symmetry of the uniform knot vector, C(b) = 0 (half-open indicator)."""
