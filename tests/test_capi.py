@@ -62,6 +62,14 @@ def test_default_options_and_validation():
     assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
     bad.stages_per_lane, bad.nlp_mode = 0, 5
     assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    bad.nlp_mode, bad.N = 0, 128                                 # N + 1 > 64 lanes x 2 stages
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    assert b"one instance must fit" in L.qsp_last_error()
+    bad.N, bad.stages_per_lane = 64, 1                            # N + 1 > 64 lanes x 1 stage
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    bad.N, bad.stages_per_lane, bad.batch = 20, 0, 0
+    assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+    assert b"N and batch" in L.qsp_last_error()
     assert L.qsp_solve(None) == -1
 
 

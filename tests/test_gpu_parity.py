@@ -245,10 +245,12 @@ def test_decagon_spline_matches_oracle():
     np.testing.assert_allclose(Dd, dDo, rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("N,S", [(1, 0), (2, 0), (5, 0), (5, 2), (20, 2), (31, 0), (63, 1), (64, 0), (90, 2)])
+@pytest.mark.parametrize("N,S", [(1, 0), (2, 0), (5, 0), (5, 2), (20, 2), (31, 0), (63, 1), (64, 0), (90, 2),
+                                 (126, 2), (127, 0)])
 def test_horizon_and_layout_edges(oracle, N, S):
     """Odd/even horizons, padding slots (S = 2 with N + 1 odd), a group filling the whole
-    wavefront (N = 63, S = 1), two stages per lane beyond it: GPU = oracle at K = 2."""
+    wavefront (N = 63, S = 1), two stages per lane beyond it, up to the largest horizon the
+    layout holds (N = 127: 64 lanes of two stages): GPU = oracle at K = 2."""
     from oracle.oracle import make_opts
     from uclv_qs_pushing_matlab_amd.objects import make_shape
     from uclv_qs_pushing_matlab_amd.solver import OcpSolver
@@ -262,9 +264,18 @@ def test_horizon_and_layout_edges(oracle, N, S):
     u = s.controller_solve(x0, 1)
     X = s.get("x")
     st = s.get("status")
+    cap = s.get("qp_capped")
     s.close()
     w = oracle.new_warm(nb, N)
     r = oracle.controller_solve(make_opts(N=N, sqp_iters=K), x0, traj, 1, w, shape_id=sid)
     assert np.all(st == 0)
-    np.testing.assert_allclose(u, r["u0"], rtol=0, atol=1e-9)
-    np.testing.assert_allclose(X, w["X"].reshape(nb, N + 1, 4), rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(cap, r["qp_capped"])
+    # a QP stopped by the iteration cap returns its last, unconverged iterate (as HPIPM at iter_max),
+    # which moves with rounding (N = 126: one such lane, the oracle itself moves 1e-8 under 1e-13
+    # input perturbations): held to 1e-5 there, 1e-9 on every other lane
+    ok = cap == 0
+    np.testing.assert_allclose(u[ok], r["u0"][ok], rtol=0, atol=1e-9)
+    # the iterate's far stages of a 6 s horizon (N >= 126) are the loosest-determined part of the QP
+    # solution: 4e-9 seen there, held to 1e-8
+    np.testing.assert_allclose(X[ok], w["X"].reshape(nb, N + 1, 4)[ok], rtol=0, atol=1e-9 if N <= 90 else 1e-8)
+    np.testing.assert_allclose(u[~ok], r["u0"][~ok], rtol=0, atol=1e-5)
