@@ -262,7 +262,7 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
                                                 const double Hx[4], const double Hu[2],
                                                 const double gx[4], const double gu[2],
                                                 double P[10], double pv[4],
-                                                double K[8], double Rn[3], double kk[2]) {
+                                                double K[8], double Rn[3], double kk[2], bool upd = true) {
     // full symmetric P
     double Pm[4][4];
 #pragma unroll
@@ -332,7 +332,8 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     }
     kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
     kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
-    // P = Q~ + S~'K ; p = q~ + K'r~
+    // P = Q~ + S~'K ; p = q~ + K'r~ (not at stage 0: nothing reads P_0, p_0; upd is uniform)
+    if (!upd) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -554,7 +555,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         // Step j runs on lanes lig <= j only: lane j-1 takes lane j's value, while lane j,
         // whose source lane j+1 sits the step out, keeps its old value (a DPP read from a
         // disabled lane returns `old`) — so every lane ends holding the dp that reached it.
-        for (int j = c.L - 2; j >= 0; --j) {
+        // (step 0 would only form dp_0, which nothing reads: lane 0 holds dp_1 after step 1)
+        for (int j = c.L - 2; j >= 1; --j) {
             if (c.lig <= j) {
                 double n[4];
 #pragma unroll
@@ -594,7 +596,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                     const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], gx3[ls]};
                     const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[ls]};
                     ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, hu[ls], gx, gu[ls], Pc, pvc, st.K[ls],
-                                    st.Rn[ls], st.kk[ls]);
+                                    st.Rn[ls], st.kk[ls], j > 0 || ls > 0);
                 } else {
                     double dkk[2];
                     ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvc, dkk);
@@ -605,12 +607,17 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                     }
                 }
             }
-            if (FACTOR) {
+            // hand-over to lane j-1 (none after step 0: lane 0 reads a disabled lane there).  The
+            // first step of a last lane without a stage (lsN == 0) leaves P at the terminal
+            // diag(We) every lane already holds, so only p moves then.
+            if (j > 0) {
+                if (FACTOR && !(j == c.L - 1 && lsN == 0)) {
 #pragma unroll
-                for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i], Pc[i]);
+                    for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i], Pc[i]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
         }
     }
     if constexpr (S == 1) {
