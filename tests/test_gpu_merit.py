@@ -106,3 +106,37 @@ def test_merit_sqp_controller_two_steps(oracle):
     d2 = np.abs(u_g2 - r2["u0"]).max(1)
     ok = st & (d < 1e-9)
     assert np.mean(d2[ok] < 1e-6) > 0.8, np.sort(d2[ok])[-6:]
+
+
+@pytest.mark.parametrize("N", [50, 63])
+def test_merit_sqp_long_horizon(oracle, N):
+    """The reference's own SQP (merit, max_iter 30) at configs[4]'s horizon and at the longest one
+    nlp_mode 1 takes (N + 1 = 64 lanes, one stage per lane), on the curved x_finals reference with a
+    per-lane start index (bench.py --config 4's input law)."""
+    from bench import SEED, config4_inputs
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    nb, K = 24, 30
+    x0, _, _, sid, traj, idx = config4_inputs(nb, N, SEED + N)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=1)
+    s = OcpSolver(N=N, batch=nb, sqp_iters=K, nlp_solver_type="SQP")
+    assert s.layout()[0] == 1
+    s.set_shapes([make_shape(n) for n in NAMES])
+    s.set_shape_ids(sid)
+    s.set_reference_trajectory(traj)
+    u_g = s.controller_solve(x0, idx)
+    status, it = s.get("status"), s.get("sqp_iter")
+    s.close()
+
+    def run(x):
+        return oracle.controller_solve(op, x, traj, idx, oracle.new_warm(nb, N), shape_id=sid)
+    r = run(x0)
+    assert set(np.unique(status)) <= {0, 2}
+    st = _stable(run, x0, r)
+    assert st.sum() >= 6, st.sum()
+    d = np.abs(u_g - r["u0"]).max(1)
+    conv = st & (r["status"] == 0) & (status == 0)
+    assert d[conv].max(initial=0.0) < 1e-6, np.sort(d[conv])[-4:]
+    assert np.mean(d[st] < 1e-6) >= 0.9, np.sort(d[st])[-4:]
+    assert np.mean(it[st] == r["iters"][st]) >= 0.9
