@@ -405,12 +405,14 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->wX, B * (N + 1) * 4 * 8);
     al(s->wU, B * N * 2 * 8);
     al(s->wx0, B * 4 * 8);
-    al(s->wlin, B * (N + 1) * 24 * 8);
     al(s->wperm, B * 4);
     al(s->wnit, B * 4);
     al(s->whist, SQP_MAX_PARTS * 4 * 1024 * 4);   // per part of the SQP loop; qsp_solver.hip PACK_KEYS_MAX
     al(s->wdone, B * 4);
     if (o->nlp_mode == QSP_NLP_SQP_MERIT) {
+        // stage data in HBM only for the line search (defect and gradient at the iterate); the
+        // fixed-K path linearises inside the QP kernel, and qsp_qp_solve stages its own
+        al(s->wlin, B * (N + 1) * 24 * 8);
         al(s->wnlp, B * (N + 1) * 20 * 8);
         al(s->wqp, B * (N + 1) * 16 * 8);
     }
