@@ -1506,7 +1506,10 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     c.inst = wave * G + c.grp;
     c.real = (c.grp < G) && (c.inst < A.nI);
-    const int iv = A.i0 + (c.real ? c.inst : A.nI - 1);
+    // the QP launch's wave packing (instances ordered by their predicted IPM count) also groups
+    // the line searches: a wave backtracks until the last of its instances accepts a step
+    const int slot = A.i0 + (c.real ? c.inst : A.nI - 1);
+    const int iv = A.wperm ? A.wperm[slot] : slot;
     const int N = p.N;
     const int k = c.lig <= N ? c.lig : N;
     const bool stg = k < N;
