@@ -47,7 +47,7 @@ struct SolveArgs {
     int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
     double* wqp;               // 16 x B(N+1)     nlp_mode 1: QP step dx(4), du(2), multipliers pi(4), lam(6), SoA
     int32_t* wperm;            // B               wave packing order of the QP kernel (nullptr: identity)
-    int32_t* wnit;             // B               IPM iterations of each instance's last two QPs (last | prev << 8)
+    int32_t* wnit;             // B               IPM iterations of each instance's last four QPs (8 bits each, last lowest)
     int32_t* whist;            // 4 x 1024        per parity of the SQP iteration: histogram of the wave-packing
                                //                 keys (accumulated by the QP kernel) and running scatter offsets
     // QP-level interface only (qsp_qp_solve): when qp_dx != nullptr the QP kernel
