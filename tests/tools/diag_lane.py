@@ -5,7 +5,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from bench import SHAPES, make_inputs  # noqa: E402
 from oracle.oracle import Oracle, make_opts  # noqa: E402
 from uclv_qs_pushing_matlab_amd.objects import make_shape  # noqa: E402

@@ -2,7 +2,7 @@
 SQP-RTI iterations (cold start each), from the library (GPU) or the oracle (--oracle), so the
 first iteration at which two implementations part can be found.
 
-  python scripts/diverge_k.py out.npz 479,651,2342 [--kmax 50] [--oracle]
+  python tests/tools/diverge_k.py out.npz 479,651,2342 [--kmax 50] [--oracle]
 """
 import argparse
 import os
@@ -10,7 +10,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 ap = argparse.ArgumentParser()
 ap.add_argument("out")

@@ -1,7 +1,7 @@
 """Developer tool: mean IPM iterations per QP, capped/failed QPs and u0 movement under changes of the
-interior-point parameters (oracle, first 1 024 bench lanes, K = 50).  Run: python scripts/ipm_param_study.py"""
+interior-point parameters (oracle, first 1 024 bench lanes, K = 50).  Run: python tests/tools/ipm_param_study.py"""
 import sys, time, numpy as np
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
 from bench import make_inputs, SEED
 from oracle.oracle import Oracle, make_opts
 o = Oracle()

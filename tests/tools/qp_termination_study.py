@@ -7,7 +7,7 @@ start, K = 50 SQP-RTI iterations) and reports
     perturbations of x0 (the oracle against itself);
   - unconverged: fraction whose u0 moves > 1e-9 between K-1 and K iterations;
   - capped: fraction of QPs stopped by the iteration cap; mean IPM iterations per QP.
-Usage: python scripts/qp_termination_study.py [lanes] [threads]
+Usage: python tests/tools/qp_termination_study.py [lanes] [threads]
 """
 import json
 import os
@@ -16,7 +16,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from bench import SHAPES, make_inputs  # noqa: E402
 from oracle.oracle import Oracle, make_opts  # noqa: E402
