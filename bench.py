@@ -144,7 +144,7 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0):
     return n, dt, r, run
 
 
-def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp):
+def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None):
     """GPU u0 vs oracle u0 on the whole CPU sample (n lanes), with the oracle's own sensitivity
     as the yardstick: a lane is chaotic when the oracle's u0 moves by > 1e-9 under
     three 1e-13 relative perturbations of x0 or when mu_stop moves 1e-10 -> 1.5e-10; parity is
@@ -164,6 +164,13 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp):
            "oracle_self_frac_le_1e-6": float(np.mean(self_dev <= 1e-6)),
            "chaotic_frac": float(np.mean(self_dev > 1e-6)),
            "qp_rule": "HPIPM-style: mu, bound, stationarity, equality residuals < 1e-10, cap 20, stall exit, stage-0 s bound"}
+    if gpu_dev is not None:
+        # the GPU's own response to the same probes: the same share of lanes moves, largely the same
+        # lanes, and the two implementations disagree almost only where one of them moves
+        gc, rc = gpu_dev[:n] > 1e-6, self_dev > 1e-6
+        out["gpu_chaotic_frac"] = float(gc.mean())
+        out["chaotic_overlap_jaccard"] = float((gc & rc).sum() / max(int((gc | rc).sum()), 1))
+        out["frac_err_gt_1e-6_stable_in_both"] = float(np.mean((d > 1e-6) & ~gc & ~rc))
     if nlp == "SQP_RTI":
         # the same statistics with round 1's QP stop rule (mu and bound residual < 1e-10, cap 20,
         # no stage-0 s bound), on the first lanes: the chaotic fraction does not depend on it
@@ -399,8 +406,17 @@ def main():
         nrep = max(1, min(args.steps, 3))
         for _ in range(nrep):
             solver.controller_reset()
-            solver.controller_solve(x0, idx_h)
+            u_host = solver.controller_solve(x0, idx_h)
         result["host_boundary_solves_per_s"] = Bl * nrep / (time.perf_counter() - th)
+        gpu_dev = None
+        if rank == 0 and not args.no_cpu and not cfg4:
+            # the GPU's own sensitivity to the parity leg's 1e-13 x0 probes (three solves, untimed)
+            gpu_dev = np.zeros(Bl)
+            for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+                solver.controller_reset()
+                gpu_dev = np.maximum(gpu_dev, np.abs(solver.controller_solve(x0 * (1 + sgn * f * 1e-13), idx_h)
+                                                     - u_host).max(1))
+            result["host_boundary_u0_equals_device_u0"] = bool(np.array_equal(u_host, u0))
     solver.close()
 
     if rank == 0 and world == 1 and not args.no_configs1 and not cfg4:
@@ -455,7 +471,7 @@ def main():
                                   "cpu_model": hc["model"],
                                   "sample": f"{n} lanes of the same workload (oracle/qsp_oracle.c, OpenMP over "
                                             f"{threads} threads, {dt:.1f} s)"}
-        result["parity"] = parity_leg(u0, x0, traj, sid, N, K, n, r, run, args.nlp)
+        result["parity"] = parity_leg(u0, x0, traj, sid, N, K, n, r, run, args.nlp, gpu_dev)
         if "configs1" in result:
             x1, traj1, sid1 = config1_inputs(N)
             from oracle.oracle import Oracle, make_opts
