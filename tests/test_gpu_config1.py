@@ -4,7 +4,8 @@ SQP-RTI iterations, cold-start NMPC_controller.solve, on the host-boundary contr
 bench's configs1 leg). Every lane is checked against the oracle with the probe criterion of
 tests/test_gpu_config2.py: on lanes whose oracle answer survives 1e-13 x0 perturbations and
 mu_stop 1.5e-10, u0 agrees within 1e-6 (BASELINE); on all lanes, the GPU agrees with the oracle
-about as often as the perturbed oracle agrees with itself."""
+about as often as the perturbed oracle agrees with itself; and the GPU's own response to the same
+perturbations marks the same lanes as chaotic, which are the lanes where the two disagree."""
 import numpy as np
 import pytest
 
@@ -23,8 +24,13 @@ def test_config1_full_batch_parity(oracle):
     s = OcpSolver(N=N, batch=B, sqp_iters=K)
     s.set_shapes([make_shape("santal")], shape_id=sid)
     s.set_reference_trajectory(traj)
-    u0 = s.controller_solve(x0, 1)
+    u0 = s.controller_solve(x0, 1).copy()
     status, capped = s.get("status"), s.get("qp_capped")
+    # the GPU's own sensitivity to the same 1e-13 x0 perturbations
+    gpu_dev = np.zeros(B)
+    for f in (1e-13, -1e-13, 3e-13):
+        s.controller_reset()
+        gpu_dev = np.maximum(gpu_dev, np.abs(s.controller_solve(x0 * (1 + f), 1) - u0).max(1))
     s.close()
     assert np.all(status == 0)
 
@@ -46,3 +52,11 @@ def test_config1_full_batch_parity(oracle):
     assert np.mean(d[nonchaotic] < 1e-6) >= 0.99, np.sort(d[nonchaotic])[-5:]
     assert np.mean(capped[nonchaotic] == ref["qp_capped"][nonchaotic]) >= 0.95
     assert np.mean(d <= 1e-6) >= np.mean(self_dev <= 1e-6) - 0.03, (np.mean(d <= 1e-6), np.mean(self_dev <= 1e-6))
+    # the disagreement is the formulation's sensitivity, seen the same way by both implementations:
+    # equal chaotic fractions (measured 10.8 % GPU, 10.9 % oracle), largely the same lanes (Jaccard
+    # 0.81), and the GPU and oracle differ by more than 1e-6 almost only where at least one of them
+    # moves under the probes (measured: 1 lane of 4 096 off while stable in both)
+    gc, rc = gpu_dev > 1e-6, self_dev > 1e-6
+    assert abs(gc.mean() - rc.mean()) < 0.02, (gc.mean(), rc.mean())
+    assert (gc & rc).sum() / max((gc | rc).sum(), 1) > 0.7
+    assert np.mean((d > 1e-6) & ~gc & ~rc) <= 0.001, np.nonzero((d > 1e-6) & ~gc & ~rc)[0][:10]
