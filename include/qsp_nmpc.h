@@ -17,6 +17,12 @@
  *               failure is NOT an error: it is the per-lane status (as acados 'status').
  *   threading : one handle per host thread; a handle owns one HIP stream on one device.
  *   precision : FP64 throughout.
+ *   versions  : qsp_version() is QSP_ABI_VERSION of the library.  Callers compiled against
+ *               this header check it before anything else; qsp_options and qsp_shape carry
+ *               their own size in struct_size (set by qsp_default_options / qsp_shape_from_ply,
+ *               or by the caller), which qsp_create and qsp_set_shapes reject when it differs
+ *               from the library's sizeof, so a stale layout fails loudly instead of being
+ *               read at the wrong offsets.
  */
 #ifndef QSP_NMPC_H
 #define QSP_NMPC_H
@@ -33,6 +39,7 @@ extern "C" {
 #define QSP_NY_E 4
 #define QSP_NH 3          /* h = [s; u_n; u_t]      (NMPC_controller.m:237) */
 #define QSP_MAX_CTRL 64   /* spline control points per shape */
+#define QSP_ABI_VERSION 2 /* 2: struct_size fields, qp_mu_max, qsp_get_qp_stalled, QP-failure exits */
 
 #define QSP_OK 0
 #define QSP_ERR_ARG (-1)
@@ -44,8 +51,10 @@ extern "C" {
 #define QSP_STATUS_SUCCESS 0
 #define QSP_STATUS_NAN 1
 #define QSP_STATUS_MAXITER 2      /* QSP_NLP_SQP_MERIT: tolerances not met within sqp_iters */
-#define QSP_STATUS_QP_FAIL 4      /* acados ACADOS_QP_FAILURE: infeasible QP (stage0_s_bound with x0's s
-                                     outside [lh_s, uh_s]); the instance does not iterate */
+#define QSP_STATUS_QP_FAIL 4      /* acados ACADOS_QP_FAILURE: an infeasible QP (stage0_s_bound with x0's s
+                                     outside [lh_s, uh_s]: the instance does not iterate) or a QP whose
+                                     interior point diverged (mu >= qp_mu_max or non-finite): the SQP
+                                     stops there with its last iterate */
 
 #define QSP_NLP_SQP_RTI_FIXED 0   /* K full Gauss-Newton steps: the BASELINE metric */
 #define QSP_NLP_SQP_MERIT 1       /* acados 'SQP' + 'merit_backtracking' with KKT tolerances
@@ -55,6 +64,7 @@ typedef struct qsp_solver qsp_solver;
 
 /* Solver options: NMPC_controller.m:270-300 (create_ocp_opts) + dims. */
 typedef struct {
+    int32_t struct_size;      /* sizeof(qsp_options) (qsp_default_options sets it)      */
     int32_t N;                /* horizon, param_scheme_N (NMPC_controller.m:281)        */
     int32_t batch;            /* number of lanes B                                      */
     int32_t nlp_mode;         /* QSP_NLP_*                                              */
@@ -80,15 +90,20 @@ typedef struct {
                                  stages 0..N-1, NMPC_controller.m:237,251-252); 0: stages 1..N-1 */
     int32_t qp_stall_iters;   /* stall exit (generalises HPIPM's alpha_min exit): a QP whose step length
                                  stays below qp_stall_alpha for qp_stall_iters consecutive iterations is
-                                 locally infeasible (mu grows without bound) and stops there, counted as
-                                 capped; default 3 x 1e-3, 0 = off (runs to qp_iters as HPIPM would) */
+                                 locally infeasible and stops there; its last iterate is used as at the
+                                 cap (qsp_get_qp_stalled counts them); default 3 x 1e-3, 0 = off */
     double qp_stall_alpha;
+    double qp_mu_max;         /* divergence exit: a QP whose complementarity mu reaches qp_mu_max (or
+                                 turns non-finite) is a QP failure (status 4, the SQP stops with its last
+                                 iterate) instead of overflowing to NaN; default 1e100 (mu starts at mu0 = 1:
+                                 an overflow guard -- QPs whose mu grows large but finite end at the stall
+                                 exit, from which the SQP recovers; measured on the bench workload) */
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */
 typedef struct {
     int32_t n_ctrl;                     /* control points, first point repeated last   */
-    int32_t pad_;
+    int32_t struct_size;                /* sizeof(qsp_shape) (qsp_shape_from_ply sets it) */
     double ctrl[QSP_MAX_CTRL][2];       /* contour points [m]                            */
     double knots[QSP_MAX_CTRL + 4];     /* clamped cubic knot vector S (n_ctrl + 4)      */
     double b;                           /* contour length (bspline_shape.m:37)           */
@@ -124,7 +139,7 @@ void qsp_default_options(qsp_options* opts);          /* N=20, B=1, K=50, Ts=0.0
 int qsp_create(const qsp_options* opts, qsp_solver** out);   /* acados_ocp(model, opts), :304 */
 int qsp_destroy(qsp_solver* s);
 const char* qsp_last_error(void);
-int qsp_version(void);
+int qsp_version(void);                                 /* QSP_ABI_VERSION */
 int qsp_get_layout(const qsp_solver* s, int32_t* stages_per_lane, int32_t* lanes_per_instance);
 
 /* ------------------------------------------------------------- model / OCP */
@@ -161,6 +176,9 @@ int qsp_get_qp_iter(qsp_solver* s, int32_t* qp_iter /* B, summed over the SQP it
 /* QPs of the last solve that stopped at the iteration cap qp_iters instead of meeting the stop
  * test (their last iterate is used, as HPIPM's at iter_max): B counts */
 int qsp_get_qp_capped(qsp_solver* s, int32_t* capped /* B */);
+/* QPs of the last solve stopped by the stall exit (qp_stall_iters steps below qp_stall_alpha;
+ * their last iterate is used as at the cap): B counts */
+int qsp_get_qp_stalled(qsp_solver* s, int32_t* stalled /* B */);
 int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
 /* dims of the handle (outputs of a MEX/FFI layer are sized from these, never from caller input) */
 int qsp_get_dims(const qsp_solver* s, int32_t* N, int32_t* B);
@@ -267,7 +285,7 @@ int qsp_eval_vbound(qsp_solver* s, int32_t n, const int32_t* shape_id, const dou
  * every stage (as in the OCP).  H: nb x (6N+4) diag, g: nb x (6N+4), lo/hi: nb x N x 3,
  * stage-0 s bound as the handle's stage0_s_bound.  qp_status (optional, nb): 0 the stop test
  * was met, 1 non-finite solution, 2 stopped at the iteration cap, 3 infeasible (the fixed
- * stage-0 s = dx0's outside its bounds). */
+ * stage-0 s = dx0's outside its bounds), 4 stall exit, 5 diverged (mu >= qp_mu_max). */
 int qsp_qp_solve(qsp_solver* s, int32_t nb, const double* A, const double* B, const double* b, const double* H,
                  const double* g, const double* lo, const double* hi, const double* dx0, double* dx, double* du,
                  double* pi, double* lam, int32_t* iters, int32_t* qp_status);

@@ -109,7 +109,9 @@ static void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[
     o.tol_eq = opt_num(op, "nlp_solver_tol_eq", 1e-6);
     o.tol_ineq = opt_num(op, "nlp_solver_tol_ineq", 1e-6);
     o.tol_comp = opt_num(op, "nlp_solver_tol_comp", 1e-6);
-    o.qp_iters = (int32_t)opt_num(op, "qp_solver_iter_max", o.qp_iters);
+    /* acados' qp_solver_iter_max default is 50 (the reference never sets it); the library's own default
+     * of 20 serves the fixed-K throughput path */
+    o.qp_iters = (int32_t)opt_num(op, "qp_solver_iter_max", o.nlp_mode == QSP_NLP_SQP_MERIT ? 50 : o.qp_iters);
     o.ls_alpha_min = opt_num(op, "globalization_alpha_min", o.ls_alpha_min);
     o.ls_alpha_red = opt_num(op, "globalization_alpha_reduction", o.ls_alpha_red);
     o.ls_eps = opt_num(op, "eps_sufficient_descent", o.ls_eps);

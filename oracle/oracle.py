@@ -2,6 +2,12 @@
 
 Loads oracle/build/libqsp_oracle.so (built by oracle/Makefile).  Used by tests/,
 __graft_entry__.smoke() and bench.py's cpu_baseline leg only.
+
+Two restatements of the reference path share one interface:
+  Oracle(...)            the literal restatement (qsp_oracle.c: full basis sum, forward AD,
+                         a dense Riccati interior point) -- pins the formulas;
+  Oracle(..., twin=True) the kernel-order twin (qsp_twin.c: the device library's formulation
+                         and operation order, explicit fma) -- reproduces the device bit for bit.
 """
 import ctypes as C
 import os
@@ -43,7 +49,8 @@ class Opts(C.Structure):
         ("ls_alpha_min", C.c_double), ("ls_alpha_red", C.c_double), ("ls_eps", C.c_double),
         ("res_stop", C.c_double),
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
-        ("qp_stall_alpha", C.c_double), ("qp_stall_iters", C.c_int32), ("pad2_", C.c_int32),
+        ("qp_stall_alpha", C.c_double), ("qp_stall_iters", C.c_int32), ("stages_per_lane", C.c_int32),
+        ("qp_mu_max", C.c_double),
     ]
 
 
@@ -52,11 +59,13 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
               lh=(-0.06, 0.0, -0.05), uh=(0.011, 0.03, 0.05),
               mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
               u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
-              qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1, qp_stall_alpha=1e-3, qp_stall_iters=3):
+              qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1, qp_stall_alpha=1e-3, qp_stall_iters=3,
+              qp_mu_max=1e100, stages_per_lane=0):
     o = Opts()
     o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, int(stage0_s_bound)
     o.qp_tol_stat, o.qp_tol_eq = qp_tol_stat, qp_tol_eq
     o.qp_stall_alpha, o.qp_stall_iters = qp_stall_alpha, int(qp_stall_iters)
+    o.qp_mu_max, o.stages_per_lane = qp_mu_max, int(stages_per_lane)
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W
@@ -79,7 +88,7 @@ def _p(a):
 
 
 class Oracle:
-    def __init__(self, names=("santal", "balea", "montana", "pulirapid"), max_ctrl=64, tab=None):
+    def __init__(self, names=("santal", "balea", "montana", "pulirapid"), max_ctrl=64, tab=None, twin=False):
         # tab: optional explicit shape table (n_ctrl, ctrl, knots, params) instead of named PLY objects
         self.tab = shape_table(names, max_ctrl) if tab is None else tab
         t = self.tab
@@ -89,6 +98,11 @@ class Oracle:
         self._pr = np.ascontiguousarray(t["params"], np.float64)
         self._mc = int(max_ctrl)
         self.L = lib()
+        self.twin = bool(twin)
+        self._pre = "tw_" if twin else "or_"
+
+    def _f(self, name):
+        return getattr(self.L, self._pre + name)
 
     def _shape_args(self):
         return (_p(self._n), _p(self._c), _p(self._k), _p(self._pr), C.c_int(self._mc))
@@ -106,6 +120,9 @@ class Oracle:
         sid = self._ids(shape_id, n)
         Cv, dC, D, dD = (np.zeros((n, 2)) for _ in range(4))
         kap = np.zeros(n)
+        if self.twin:   # (C, C', C'', kappa): the device's spline outputs
+            self.L.tw_spline_eval(*self._shape_args(), C.c_int32(n), _p(sid), _p(s), _p(Cv), _p(D), _p(dD), _p(kap))
+            return Cv, D, dD, kap
         self.L.or_spline_eval(*self._shape_args(), C.c_int32(n), _p(sid), _p(s), _p(Cv), _p(dC), _p(D), _p(dD), _p(kap))
         return Cv, dC, D, dD, kap
 
@@ -116,7 +133,7 @@ class Oracle:
         sid = self._ids(shape_id, n)
         f = np.zeros((n, 4))
         J = np.zeros((n, 4, 6))
-        self.L.or_dynamics(*self._shape_args(), C.c_int32(n), _p(sid), _p(x), _p(u), _p(f), _p(J))
+        self._f('dynamics')(*self._shape_args(), C.c_int32(n), _p(sid), _p(x), _p(u), _p(f), _p(J))
         return f, J
 
     def rk4(self, x, u, h=0.05, shape_id=None):
@@ -127,7 +144,7 @@ class Oracle:
         xn = np.zeros((n, 4))
         A = np.zeros((n, 4, 4))
         B = np.zeros((n, 4, 2))
-        self.L.or_rk4(*self._shape_args(), C.c_int32(n), _p(sid), C.c_double(h), _p(x), _p(u), _p(xn), _p(A), _p(B))
+        self._f('rk4')(*self._shape_args(), C.c_int32(n), _p(sid), C.c_double(h), _p(x), _p(u), _p(xn), _p(A), _p(B))
         return xn, A, B
 
     def vbound(self, s, opts, shape_id=None):
@@ -135,7 +152,7 @@ class Oracle:
         n = len(s)
         sid = self._ids(shape_id, n)
         vb = np.zeros(n)
-        self.L.or_vbound(*self._shape_args(), C.byref(opts), C.c_int32(n), _p(sid), _p(s), _p(vb))
+        self._f('vbound')(*self._shape_args(), C.byref(opts), C.c_int32(n), _p(sid), _p(s), _p(vb))
         return vb
 
     def qp(self, opts, A, B, b, H, g, lo, hi, act, dx0):
@@ -150,7 +167,7 @@ class Oracle:
         lam = np.zeros((nb, N, 6))
         iters = np.zeros(nb, np.int32)
         qst = np.zeros(nb, np.int32)
-        r = self.L.or_qp_batch(C.byref(opts), C.c_int32(nb), *[_p(a) for a in arrs], _p(act), _p(dx0),
+        r = self._f('qp_batch')(C.byref(opts), C.c_int32(nb), *[_p(a) for a in arrs], _p(act), _p(dx0),
                                _p(dx), _p(du), _p(pi), _p(lam), _p(iters), _p(qst))
         return dict(dx=dx, du=du, pi=pi, lam=lam, iters=iters, fail=r, qp_status=qst)
 
@@ -170,18 +187,25 @@ class Oracle:
         qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
         capped = np.zeros(nb, np.int32)
-        self.L.or_ocp_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
-                            _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                            C.c_int(nthreads), _p(capped))
-        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
+        stalled = np.zeros(nb, np.int32)
+        self._f("ocp_solve")(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
+                             _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(qp_iter), _p(cost),
+                             C.c_int(nthreads), _p(capped), _p(stalled))
+        return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped,
+                    qp_stalled=stalled)
 
     def controller_solve(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0, delay_cols=0):
-        """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place."""
+        """warm: dict with X (nb,N+1,4), U (nb,N,2), PI (nb,N,4), valid (nb,) uint8 — updated in place.
+        traj: (T, 6) shared, or (nb, T, 6) per lane (twin only)."""
         N = opts.N
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
         nb = len(x0)
         sid = self._ids(shape_id, nb)
-        traj = np.ascontiguousarray(traj, np.float64).reshape(-1, 6)
+        per_lane = np.ndim(traj) == 3
+        if per_lane and not self.twin:
+            raise ValueError("per-lane reference tables: twin only")
+        traj = np.ascontiguousarray(traj, np.float64)
+        T = traj.shape[1] if per_lane else traj.reshape(-1, 6).shape[0]
         idx = np.ascontiguousarray(np.broadcast_to(np.asarray(index_time, np.int32), (nb,)), np.int32)
         u0 = np.zeros((nb, 2))
         status = np.zeros(nb, np.int32)
@@ -189,14 +213,18 @@ class Oracle:
         qp_iter = np.zeros(nb, np.int32)
         cost = np.zeros(nb)
         capped = np.zeros(nb, np.int32)
-        self.L.or_controller_solve(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
-                                   C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]),
-                                   _p(warm["valid"]), _p(u0), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                                   C.c_int(nthreads), _p(capped), C.c_int32(int(delay_cols)))
-        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped)
+        stalled = np.zeros(nb, np.int32)
+        args = [*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj), C.c_int32(T), _p(idx),
+                _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]), _p(warm["valid"]), _p(u0), _p(status), _p(iters),
+                _p(qp_iter), _p(cost), C.c_int(nthreads), _p(capped), C.c_int32(int(delay_cols))]
+        if self.twin:
+            self.L.tw_controller_solve(*args, C.c_int32(int(per_lane)), _p(stalled))
+        else:
+            self.L.or_controller_solve(*args, _p(stalled))
+        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped, qp_stalled=stalled)
 
     def closed_loop(self, opts, x0, traj, n_steps, index0=1, shape_id=None, noise=None, delay_cols=0,
-                    plant_delay_cols=0, dist_step=0, dist_amp=None, xwidth=None, nthreads=0):
+                    plant_delay_cols=0, dist_step=0, dist_amp=None, xwidth=None, nthreads=0, ubc0=None):
         """helper.m:195-322 closed loop (see or_closed_loop).  Returns X (nb, n+1, 4), Xsim (nb, n, 4),
         U (nb, n, 2), status (nb, n)."""
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
@@ -211,10 +239,17 @@ class Oracle:
         Xs = np.zeros((nb, n, 4))
         U = np.zeros((nb, n, 2))
         st = np.zeros((nb, n), np.int32)
-        r = self.L.or_closed_loop(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
-                                  C.c_int32(len(traj)), _p(idx), C.c_int32(n), None if nz is None else _p(nz),
-                                  C.c_int32(int(delay_cols)), C.c_int32(int(plant_delay_cols)), C.c_int32(int(dist_step)),
-                                  _p(amp), _p(xw), _p(X), _p(Xs), _p(U), _p(st), C.c_int(nthreads))
+        args = [*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
+                C.c_int32(len(traj)), _p(idx), C.c_int32(n), None if nz is None else _p(nz),
+                C.c_int32(int(delay_cols)), C.c_int32(int(plant_delay_cols)), C.c_int32(int(dist_step)),
+                _p(amp), _p(xw), _p(X), _p(Xs), _p(U), _p(st), C.c_int(nthreads)]
+        if self.twin:   # ubc0: the controller's input buffer at the start (B x delay_cols x 2; None: zeros)
+            u0b = None if ubc0 is None else np.ascontiguousarray(ubc0, np.float64).reshape(nb, int(delay_cols), 2)
+            r = self.L.tw_closed_loop(*args, None if u0b is None else _p(u0b))
+        else:
+            if ubc0 is not None:
+                raise ValueError("ubc0: twin only")
+            r = self.L.or_closed_loop(*args)
         if r != 0:
             raise ValueError("or_closed_loop: bad arguments")
         return dict(X=X, Xsim=Xs, U=U, status=st)
@@ -226,7 +261,7 @@ class Oracle:
         s0 = np.ascontiguousarray(np.broadcast_to(s0, (n,)), np.float64)
         sid = self._ids(shape_id, n)
         s = np.zeros(n)
-        self.L.or_reproject_contact(*self._shape_args(), C.c_int32(n), _p(sid), _p(px), _p(py), _p(s0), _p(s))
+        self._f('reproject_contact')(*self._shape_args(), C.c_int32(n), _p(sid), _p(px), _p(py), _p(s0), _p(s))
         return s
 
     @staticmethod

@@ -53,46 +53,7 @@ typedef struct {
     double mu;          /* mu_sp */
 } or_shape;
 
-/* -------------------------------------------------------------- options */
-typedef struct {
-    int32_t N;          /* horizon (param_scheme_N) */
-    int32_t sqp_iters;  /* K full Gauss-Newton steps */
-    int32_t qp_iters;   /* Mehrotra iterations per QP */
-    int32_t stage0_s_bound; /* 1: the s bound of h also applies at stage 0 (acados-recall: bgh at
-                               stage 0, NMPC_controller.m:237,251-252); s_0 is fixed by x0, so an
-                               x0 with s outside [lh_s, uh_s] makes every QP infeasible */
-    double Ts;          /* h = T/N */
-    double tau;         /* stage-cost scaling (acados: Ts) */
-    double W[6];        /* diag(blkdiag(W_x, W_u))   (NMPC_controller.m:157, main.m:82-86) */
-    double We[4];       /* diag(W_x_e)               (NMPC_controller.m:154) */
-    double lh[3], uh[3];/* bounds on h = [s; u_n; u_t] (NMPC_controller.m:251-252) */
-    double mu0;         /* IPM initial complementarity */
-    double t_min;       /* IPM slack floor at initialisation */
-    double frac;        /* fraction to boundary */
-    double sigma_min;   /* lower clamp of the Mehrotra centering parameter */
-    double mu_stop;     /* per-QP early exit once mu < mu_stop */
-    double v_alpha, d_v, t_angle0; /* NMPC_controller.m:98-100 */
-    double u_n_lb, u_t_ub;         /* NMPC_controller.m:23-26 */
-    /* globalised SQP (nlp_mode == 1): acados "sqp" + "merit_backtracking",
-     * tolerances nlp_solver_tol_* (NMPC_controller.m:271-276) */
-    int32_t nlp_mode;   /* 0: fixed-K full-step (RTI metric), 1: SQP + merit line search + tolerances */
-    int32_t pad_;
-    double tol_stat, tol_eq, tol_ineq, tol_comp;
-    double ls_alpha_min, ls_alpha_red, ls_eps;
-    double res_stop;    /* per-QP early exit also needs the bound residual below res_stop */
-    /* HPIPM-style QP termination (ocp_qp_ipm: res_g, res_b next to res_d = res_stop and
-     * res_m = mu_stop): the stationarity and equality residuals of the IPM iterate.  Both are
-     * linear in the iterate and every Newton step solves them exactly, so each update scales
-     * them by (1 - alpha): tracked as r_0 * prod(1 - alpha) from the start point (z = 0, pi = 0,
-     * lam = mu0 / t), like the bound residual. */
-    double qp_tol_stat, qp_tol_eq;
-    /* stall exit: a QP whose step length stays below qp_stall_alpha for qp_stall_iters
-     * consecutive iterations is locally infeasible (e.g. the linearised s dynamics cannot meet
-     * the s bound): mu grows without bound and alpha ~1e-5 to the cap.  It stops there, with
-     * the capped QPs' status (its last iterate is used, as at the cap).  0 iterations: off. */
-    double qp_stall_alpha;
-    int32_t qp_stall_iters, pad2_;
-} or_opts;
+#include "or_opts.h"
 
 /* ================================================================ dual numbers */
 typedef struct { double v, d[NDIR]; } dual;
@@ -430,7 +391,9 @@ static inline double bnd_val(const double *dx, const double *du, int k, int j)
 
 /* Mehrotra predictor-corrector IPM.  Returns 0 (stop test met), 1 (non-finite solution),
  * 2 (iteration cap reached first: the last iterate is returned, as HPIPM at iter_max),
- * 3 (infeasible: a fixed bounded component, the stage-0 s = x0's s, lies outside its bounds). */
+ * 3 (infeasible: a fixed bounded component, the stage-0 s = x0's s, lies outside its bounds),
+ * 4 (stall exit: the last iterate is returned as at the cap), 5 (diverged: mu reached
+ * qp_mu_max or turned non-finite -- a QP failure, acados ACADOS_QP_FAILURE). */
 static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, double *work, int *nit_out)
 {
     int N = qp->N;
@@ -483,17 +446,19 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     double rs_stop = o->res_stop / r0;
     if (o->qp_tol_stat / rg0 < rs_stop) rs_stop = o->qp_tol_stat / rg0;
     if (o->qp_tol_eq / rb0 < rs_stop) rs_stop = o->qp_tol_eq / rb0;
-    int nit = 0, converged = 0, stall = 0;
+    int nit = 0, converged = 0, stall = 0, stalled = 0, diverged = 0;
     for (int it = 0; it <= o->qp_iters && !infeasible; ++it) {
         double mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
         mu /= (double)m;
+        /* divergence (multipliers growing without bound; a NaN mu would pass the stop test) */
+        if (!(mu < o->qp_mu_max)) { diverged = 1; break; }
         /* HPIPM's four exit residuals: complementarity, and the bound, stationarity and equality
          * residuals r0, rg0, rb0 times their common scale prod(1 - alpha) -- tested as
          * prod < min(tol / r) (x / 0 = inf: a residual that starts at zero never binds) */
         if (!(mu >= o->mu_stop) && !(rscale >= rs_stop)) { converged = 1; break; }
         if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
-        if (o->qp_stall_iters > 0 && stall >= o->qp_stall_iters) break;   /* stalled: as at the cap */
+        if (o->qp_stall_iters > 0 && stall >= o->qp_stall_iters) { stalled = 1; break; }   /* as at the cap */
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
@@ -593,7 +558,8 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(sol->dx[q])) return 1;
     for (int q = 0; q < 2 * N; ++q) if (!isfinite(sol->du[q])) return 1;
     if (infeasible) return 3;
-    return converged ? 0 : 2;
+    if (diverged) return 5;
+    return converged ? 0 : (stalled ? 4 : 2);
 }
 
 /* ================================================================ SQP */
@@ -608,6 +574,7 @@ typedef struct {
     or_fact F;
     int qp_total;
     int qp_capped;   /* QPs of this solve stopped by the iteration cap */
+    int qp_stalled;  /* ... by the stall exit */
 } or_ws;
 
 static double ocp_cost(const or_opts *o, int N, const double *X, const double *U, const double *yref, const double *yref_e)
@@ -743,9 +710,10 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         const int qst = qp_solve(&qp, o, &sol, &ws->F, ws->work, &nit);
         ws->qp_total += nit;
         if (qst == 2) ws->qp_capped++;
-        /* non-finite QP solution: status 1; infeasible QP: status 4 (acados ACADOS_QP_FAILURE);
-         * either way the SQP stops with its last finite iterate */
-        if (qst == 1 || qst == 3) { status = qst == 1 ? 1 : 4; break; }
+        if (qst == 4) ws->qp_stalled++;
+        /* non-finite QP solution: status 1; infeasible or diverged QP: status 4 (acados
+         * ACADOS_QP_FAILURE); either way the SQP stops with its last finite iterate */
+        if (qst == 1 || qst == 3 || qst == 5) { status = qst == 1 ? 1 : 4; break; }
         double alpha = 1.0;
         if (o->nlp_mode == 1) {
             /* merit weights (acados: max(|mult|, (weight + |mult|)/2)) */
@@ -900,7 +868,7 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
                  int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
                  const double *x0, const double *yref, const double *yref_e,
                  double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
-                 double *cost, int nthreads, int32_t *qp_capped)
+                 double *cost, int nthreads, int32_t *qp_capped, int32_t *qp_stalled)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -917,9 +885,11 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
             const double *yr = yref + (size_t)i * 6 * N, *ye = yref_e + (size_t)i * 4;
             ws->qp_total = 0;
             ws->qp_capped = 0;
+            ws->qp_stalled = 0;
             status[i] = sqp_solve(&sh, o, x0 + 4 * i, yr, ye, Xi, Ui, Pi, lam ? lam + (size_t)i * 6 * N : NULL, iters ? iters + i : NULL, ws);
             if (qp_iter) qp_iter[i] = ws->qp_total;
             if (qp_capped) qp_capped[i] = ws->qp_capped;
+            if (qp_stalled) qp_stalled[i] = ws->qp_stalled;
             cost[i] = ocp_cost(o, N, Xi, Ui, yr, ye);
         }
         free(ws);
@@ -949,7 +919,7 @@ static void ref_column(const double *traj, int32_t T, int32_t D, int c, double o
 static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0_in[4], const double *traj,
                            int32_t T, int32_t D, int32_t index_time, double *X, double *U, double *PI,
                            uint8_t *warm_valid, double u0[2], int32_t *iters, int32_t *qp_iter, int32_t *qp_capped,
-                           double *cost, or_ws *ws)
+                           double *cost, or_ws *ws, int32_t *qp_stalled)
 {
     int N = o->N;
     if (N < 1 || N > OR_MAX_N) return 1;
@@ -991,9 +961,11 @@ static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0
     /* :389 solve */
     ws->qp_total = 0;
     ws->qp_capped = 0;
+    ws->qp_stalled = 0;
     int status = sqp_solve(sh, o, x0, yref, ye, X, U, PI, NULL, iters, ws);
     if (qp_iter) *qp_iter = ws->qp_total;
     if (qp_capped) *qp_capped = ws->qp_capped;
+    if (qp_stalled) *qp_stalled = ws->qp_stalled;
     if (cost) *cost = ocp_cost(o, N, X, U, yref, ye);
     u0[0] = U[0]; u0[1] = U[1];
     /* :397-399 shift (duplicate last column) */
@@ -1015,7 +987,7 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                         const double *x0_in, const double *traj, int32_t T, const int32_t *index_time,
                         double *Xw, double *Uw, double *PIw, uint8_t *warm_valid,
                         double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads,
-                        int32_t *qp_capped, int32_t delay_cols)
+                        int32_t *qp_capped, int32_t delay_cols, int32_t *qp_stalled)
 {
     int N = o->N;
     if (N > OR_MAX_N) return -1;
@@ -1031,7 +1003,7 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
             status[i] = ctrl_solve_lane(&sh, o, x0_in + 4 * i, traj, T, delay_cols, index_time[i],
                                         Xw + (size_t)i * 4 * (N + 1), Uw + (size_t)i * 2 * N, PIw + (size_t)i * 4 * N,
                                         warm_valid + i, u0 + 2 * i, iters ? iters + i : NULL, qp_iter ? qp_iter + i : NULL,
-                                        qp_capped ? qp_capped + i : NULL, cost + i, ws);
+                                        qp_capped ? qp_capped + i : NULL, cost + i, ws, qp_stalled ? qp_stalled + i : NULL);
         }
         free(ws);
     }
@@ -1139,7 +1111,7 @@ int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
                 if (Xsim) memcpy(Xsim + ((size_t)i * n_steps + t) * 4, xs, sizeof xs);
                 double u[2];
                 const int st = ctrl_solve_lane(&sh, o, xs, traj, T, delay_cols, index0[i] + t + delay_cols, X, U, PI,
-                                               &valid, u, NULL, NULL, NULL, NULL, ws);
+                                               &valid, u, NULL, NULL, NULL, NULL, ws, NULL);
                 if (delay_cols > 0) {                         /* u_buff_contr = [u, u_buff_contr(:, 1:end-1)] */
                     memmove(ubc + 2, ubc, sizeof(double) * 2 * (size_t)(delay_cols - 1));
                     ubc[0] = u[0]; ubc[1] = u[1];

@@ -1,0 +1,229 @@
+"""Bit-exact GPU parity: the HIP library against the oracle's kernel-order twin (oracle/qsp_twin.c).
+
+The library is built with -ffp-contract=off and writes every fused multiply-add out; the twin
+restates the same reference path (PusherSliderModel.m:503-603, bspline_shape.m:40-152, the acados
+SQP/HPIPM algorithms of NMPC_controller.m:270-300, the solve wrapper :329-423, helper.m:195-322)
+in the same formulation and operation order on the CPU.  Every operation involved is IEEE-exact
+on both sides (scripts/ubench/fp_exact.hip), so the expected result is equality of every bit, on
+every lane -- including the lanes where the fixed-K full-step SQP is chaotic, where
+any rounding-level difference would show.  Tolerance: none (np.array_equal, NaN == NaN).
+"""
+import numpy as np
+import pytest
+
+from conftest import config2_x0, straight_traj
+from qp_data import build_qp
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+def same(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    eq = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+    if not eq.all():
+        bad = np.argwhere(~eq)
+        i = tuple(bad[0])
+        raise AssertionError(f"{what}: {len(bad)} of {a.size} entries differ; first at {i}: gpu {a[i]!r} twin {b[i]!r}")
+
+
+@pytest.fixture(scope="module")
+def twin():
+    from oracle.oracle import Oracle
+    return Oracle(NAMES, twin=True)
+
+
+def solver(N, B, **kw):
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    s = OcpSolver(N=N, batch=B, **kw)
+    s.set_shapes([make_shape(n) for n in NAMES])
+    return s
+
+
+def test_building_blocks_bit_identical(twin):
+    from oracle.oracle import make_opts
+    s = solver(20, 64)
+    rng = np.random.default_rng(11)
+    n = 4000
+    for sid in range(4):
+        b = twin.tab["params"][sid, 0]
+        knots = twin.tab["knots"][sid, :twin.tab["n_ctrl"][sid] + 4]
+        sig = np.concatenate([rng.uniform(-0.1 * b, 1.1 * b, n), knots, [b, np.nextafter(b, 0), 0.0, -0.0]])
+        for g, t, name in zip(s.eval_spline(sig, sid), twin.spline(sig, sid), ("C", "D", "Dd", "kappa")):
+            same(g, t, f"spline {name} shape {sid}")
+        x = np.stack([rng.uniform(-0.05, 0.05, n), rng.uniform(-0.05, 0.05, n), rng.uniform(-7.0, 7.0, n),
+                      rng.uniform(-1.5 * b, 1.5 * b, n)], 1)
+        u = np.stack([rng.uniform(0.0, 0.03, n), rng.uniform(-0.05, 0.05, n)], 1)
+        u[:40] = 0.0
+        u[40:80, 0] = 0.0
+        for g, t, name in zip(s.eval_dynamics(x, u, sid), twin.dynamics(x, u, sid), ("f", "J")):
+            same(g, t, f"dynamics {name} shape {sid}")
+        for g, t, name in zip(s.eval_rk4(x, u, 0.05, sid), twin.rk4(x, u, 0.05, sid), ("xn", "A", "B")):
+            same(g, t, f"rk4 {name} shape {sid}")
+        sv = rng.uniform(-2 * b, 2 * b, n)
+        same(s.eval_vbound(sv, sid), twin.vbound(sv, make_opts(), sid), f"v_bound shape {sid}")
+    s.close()
+
+
+@pytest.mark.parametrize("N,S", [(20, 1), (20, 2), (50, 2)])
+def test_qp_bit_identical(twin, N, S):
+    """qsp_qp_solve against the twin's QP on the OCP's Gauss-Newton QPs at perturbed iterates
+    (both lane layouts: their recursions associate differently, and each must match its own)."""
+    from oracle.oracle import make_opts
+    rng = np.random.default_rng(5 + N + S)
+    nb = 192
+    op = make_opts(N=N, stages_per_lane=S)
+    x0 = config2_x0(nb, 17 + N)
+    X = np.repeat(x0[:, None], N + 1, 1) + rng.normal(0, 2e-3, (nb, N + 1, 4))
+    U = np.stack([rng.uniform(0, 0.03, (nb, N)), rng.uniform(-0.02, 0.02, (nb, N))], 2)
+    traj = straight_traj()
+    yref = np.broadcast_to(traj[None, :N], (nb, N, 6)).copy()
+    sid = np.arange(nb) % 4
+    A, B, b, H, g, lo, hi, act, dx0 = build_qp(twin, op, X, U, yref, yref[:, -1, :4], x0, sid)
+    s = solver(N, nb, stages_per_lane=S)
+    assert s.layout()[0] == S
+    r = s.qp_solve(A.reshape(nb, N, 16), B.reshape(nb, N, 8), b, H, g, lo, hi, dx0)
+    s.close()
+    t = twin.qp(op, A.reshape(nb, N, 16), B.reshape(nb, N, 8), b, H, g, lo, hi, act, dx0)
+    for k in ("dx", "du", "pi", "lam", "iters", "qp_status"):
+        same(r[k], t[k], f"qp {k}")
+    assert np.mean(t["qp_status"] == 0) > 0.9
+
+
+def controller_pair(twin, N, B, x0, traj, sid, idx, K=50, steps=1, **kw):
+    """Cold-start controller solves (then warm-started repeats) on the GPU and on the twin."""
+    from oracle.oracle import make_opts
+    nlp = kw.pop("nlp_mode", 0)
+    s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI", **kw)
+    s.set_shape_ids(sid)
+    s.set_reference_trajectory(traj)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp, qp_iters=kw.get("qp_iters", 20), qp_mu_max=kw.get("qp_mu_max", 1e100))
+    warm = twin.new_warm(B, N)
+    for step in range(steps):
+        u = s.controller_solve(x0, idx + step)
+        r = twin.controller_solve(op, x0, traj, idx + step, warm, shape_id=sid)
+        same(u, r["u0"], f"u0 (step {step})")
+        for f in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
+            same(s.get(f), r[{"sqp_iter": "iters"}.get(f, f)], f"{f} (step {step})")
+        same(s.get("x"), warm["X"], f"warm X (step {step})")
+        same(s.get("u"), warm["U"], f"warm U (step {step})")
+        same(s.get("pi"), warm["PI"], f"warm PI (step {step})")
+        same(s.get_cost(), r["cost"], f"cost (step {step})")
+    s.close()
+    return r
+
+
+def test_configs1_full_batch_bit_identical(twin):
+    """BASELINE configs[1] (B = 4 096 santal lanes, N = 20, K = 50): every lane, every output."""
+    from bench import config1_inputs
+    x0, traj, sid = config1_inputs(20)
+    r = controller_pair(twin, 20, len(x0), x0, traj, sid, 1)
+    assert np.mean(r["status"] == 0) > 0.99
+
+
+def test_bench_workload_bit_identical(twin):
+    """BASELINE configs[2] (the headline): all 65 536 lanes, 4 shapes mixed, K = 50, then one
+    warm-started step (shifted warm start, y_ref from index 2)."""
+    from bench import CONFIG2_BATCH, SEED, make_inputs
+    x0, _, _, sid, traj = make_inputs(CONFIG2_BATCH, 20, SEED)
+    controller_pair(twin, 20, CONFIG2_BATCH, x0, traj, sid, 1, steps=2)
+
+
+def test_configs4_bit_identical(twin):
+    """BASELINE configs[4]: N = 50 (two stages per lane), B = 16 384, the curved x_finals reference
+    with a random start index per lane."""
+    from bench import SEED, config4_inputs
+    x4, _, _, sid4, traj4, idx4 = config4_inputs(16384, 50, SEED)
+    controller_pair(twin, 50, len(x4), x4, traj4, sid4, idx4)
+
+
+def test_merit_sqp_bit_identical(twin):
+    """The reference's own solver configuration (sqp + merit_backtracking, max_iter 30, tol 1e-6,
+    NMPC_controller.m:271-276) on 4 096 configs[2] lanes: statuses, iteration counts, u0, the
+    NLP multipliers; two controller steps (the second warm-started from the shifted solution)."""
+    from bench import SEED, make_inputs
+    x0, _, _, sid, traj = make_inputs(4096, 20, SEED + 7)
+    r = controller_pair(twin, 20, 4096, x0, traj, sid, 1, K=30, steps=2, nlp_mode=1)
+    assert np.mean(r["status"] == 0) > 0.15   # tol 1e-6 within 30 iterations: about a quarter of these lanes (both)
+
+
+def test_small_batch_fused_loop_bit_identical(twin):
+    """B = 960 runs the whole SQP loop in one launch (sqp_loop_kernel); same bits as the twin."""
+    from bench import SEED, make_inputs
+    x0, _, _, sid, traj = make_inputs(960, 20, SEED + 3)
+    controller_pair(twin, 20, 960, x0, traj, sid, 1)
+
+
+def test_acados_level_solve_bit_identical(twin):
+    """qsp_solve ('constr_x0', 'cost_y_ref', 'init_x/u/pi', .solve()) in both NLP modes."""
+    from oracle.oracle import make_opts
+    N, B = 20, 512
+    rng = np.random.default_rng(3)
+    x0 = config2_x0(B, 99)
+    traj = straight_traj()
+    yref = np.broadcast_to(traj[None, 3:3 + N], (B, N, 6)).copy()
+    ye = yref[:, -1, :4].copy()
+    X = np.repeat(x0[:, None], N + 1, 1) + rng.normal(0, 1e-3, (B, N + 1, 4))
+    U = np.stack([rng.uniform(0, 0.02, (B, N)), rng.uniform(-0.01, 0.01, (B, N))], 2)
+    PI = rng.normal(0, 1e-3, (B, N, 4))
+    sid = np.arange(B) % 4
+    for nlp, K in ((0, 10), (1, 30)):
+        s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI")
+        s.set_shape_ids(sid)
+        s.set("constr_x0", x0)
+        s.set("cost_y_ref", yref)
+        s.set("cost_y_ref_e", ye)
+        s.set("init_x", X)
+        s.set("init_u", U)
+        s.set("init_pi", PI)
+        s.solve()
+        r = twin.ocp_solve(make_opts(N=N, sqp_iters=K, nlp_mode=nlp), x0, yref, ye, X, U, PI, shape_id=sid)
+        same(s.get("x"), r["X"], f"x (nlp {nlp})")
+        same(s.get("u"), r["U"], f"u (nlp {nlp})")
+        same(s.get("pi"), r["PI"], f"pi (nlp {nlp})")
+        for f in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
+            same(s.get(f), r[{"sqp_iter": "iters"}.get(f, f)], f"{f} (nlp {nlp})")
+        same(s.get_cost(), r["cost"], f"cost (nlp {nlp})")
+        s.close()
+
+
+def test_closed_loop_bit_identical(twin):
+    """helper.closed_loop_matlab on the device (sim_noise, controller delay compensation 0.1 s,
+    plant delay 0.05 s, a disturbance with contact re-projection at step 6) against the twin."""
+    from oracle.oracle import make_opts
+    from uclv_qs_pushing_matlab_amd.objects import object_selection
+    N, B, T = 20, 256, 12
+    x0 = config2_x0(B, 7)
+    traj = straight_traj()
+    sid = np.arange(B) % 4
+    noise = np.random.default_rng(1).standard_normal((T, B, 4)) * np.array([1e-5, 1e-5, 1e-3, 1e-4])
+    amp = np.random.default_rng(2).uniform(-0.004, 0.004, B)
+    s = solver(N, B, sqp_iters=5)
+    s.set_shape_ids(sid)
+    s.set_reference_trajectory(traj)
+    s.set_delay_comp(0.1)
+    D = s.delay_cols()
+    g = s.closed_loop(x0, T, noise=noise, plant_delay=0.05, disturbance=True, t_dist=6, amplitude=amp)
+    s.close()
+    xw = np.array([object_selection(n)["xwidth"] for n in NAMES])
+    t = twin.closed_loop(make_opts(N=N, sqp_iters=5), x0, traj, T, shape_id=sid, noise=noise, delay_cols=D,
+                         plant_delay_cols=1, dist_step=6, dist_amp=amp, xwidth=xw)
+    for k in ("X", "Xsim", "U", "status"):
+        same(g[k], t[k], f"closed loop {k}")
+
+
+@pytest.mark.parametrize("mu_max", [0.5, 1e6])
+def test_qp_divergence_exit_bit_identical(twin, mu_max):
+    """The QP-failure exit (mu >= qp_mu_max: status 4, the SQP stops with its last iterate) on the
+    same lanes as the twin: at 0.5 (< mu0) every lane's first QP fails (sqp_iter 0, u0 = the warm-start
+    rollout's), at 1e6 a mixture (about 1 % of these lanes' QPs reach it)."""
+    from bench import SEED, make_inputs
+    x0, _, _, sid, traj = make_inputs(4096, 20, SEED + 11)
+    r = controller_pair(twin, 20, 4096, x0, traj, sid, 1, qp_mu_max=mu_max)
+    if mu_max < 1.0:
+        assert np.all(r["status"] == 4) and np.all(r["iters"] == 0)
+    else:
+        assert 0 < np.sum(r["status"] == 4) < 200

@@ -12,6 +12,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 # QSP_LIB_PATH: developer override (A/B runs of differently compiled libraries)
 LIB_PATH = os.environ.get("QSP_LIB_PATH") or os.path.join(_PKG, "libqsp_nmpc.so")
 MAX_CTRL = 64
+ABI_VERSION = 2   # include/qsp_nmpc.h QSP_ABI_VERSION
 
 _lib = None
 
@@ -22,7 +23,7 @@ class QspError(RuntimeError):
 
 class Options(C.Structure):
     _fields_ = [
-        ("N", C.c_int32), ("batch", C.c_int32), ("nlp_mode", C.c_int32), ("sqp_iters", C.c_int32),
+        ("struct_size", C.c_int32), ("N", C.c_int32), ("batch", C.c_int32), ("nlp_mode", C.c_int32), ("sqp_iters", C.c_int32),
         ("qp_iters", C.c_int32), ("stages_per_lane", C.c_int32), ("device", C.c_int32), ("cost_scale_Ts", C.c_int32),
         ("Ts", C.c_double), ("mu0", C.c_double), ("t_min", C.c_double), ("frac", C.c_double),
         ("sigma_min", C.c_double), ("mu_stop", C.c_double),
@@ -31,16 +32,21 @@ class Options(C.Structure):
         ("res_stop", C.c_double),
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
         ("stage0_s_bound", C.c_int32), ("qp_stall_iters", C.c_int32), ("qp_stall_alpha", C.c_double),
+        ("qp_mu_max", C.c_double),
     ]
 
 
 class Shape(C.Structure):
     _fields_ = [
-        ("n_ctrl", C.c_int32), ("pad_", C.c_int32),
+        ("n_ctrl", C.c_int32), ("struct_size", C.c_int32),
         ("ctrl", (C.c_double * 2) * MAX_CTRL),
         ("knots", C.c_double * (MAX_CTRL + 4)),
         ("b", C.c_double), ("c_ellipse", C.c_double), ("mu_sp", C.c_double), ("xwidth", C.c_double),
     ]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        self.struct_size = C.sizeof(Shape)   # qsp_set_shapes checks the layout (ABI v2)
 
 
 class ClosedLoopOpts(C.Structure):
@@ -85,6 +91,7 @@ _SIGS = {
     "qsp_get_sqp_iter": [_P, _P],
     "qsp_get_qp_iter": [_P, _P],
     "qsp_get_qp_capped": [_P, _P],
+    "qsp_get_qp_stalled": [_P, _P],
     "qsp_get_time_tot": [_P, C.POINTER(_D)],
     "qsp_get_dims": [_P, C.POINTER(_I), C.POINTER(_I)],
     "qsp_set_yref_stage": [_P, _I, _P],
@@ -140,6 +147,9 @@ def lib():
     except ImportError:
         pass
     L = C.CDLL(LIB_PATH)
+    L.qsp_version.restype = C.c_int
+    if L.qsp_version() != ABI_VERSION:
+        raise QspError(f"{LIB_PATH}: ABI version {L.qsp_version()}, this binding needs {ABI_VERSION} (rebuild)")
     for name, args in _SIGS.items():
         fn = getattr(L, name)
         fn.argtypes = args

@@ -11,7 +11,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libqsp_nmpc.so")
 SOURCES = ["qsp_solver.hip", "qsp_capi.hip"]
-HEADERS = ["qsp_math.hpp", "qsp_types.h", "qsp_kernels.h", "../../include/qsp_nmpc.h"]
+HEADERS = ["qsp_math.hpp", "qsp_fp.hpp", "qsp_types.h", "qsp_kernels.h", "../../include/qsp_nmpc.h"]
 ARCH = os.environ.get("QSP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -27,7 +27,9 @@ def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -ffp-contract=off: every fused multiply-add is an explicit fma() in the source, so the
+    # oracle twin reproduces the device arithmetic bit for bit (qsp_fp.hpp)
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
            "-I", os.path.join(PKG, "..", "include")]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     cmd += ["-o", LIB + ".tmp"]

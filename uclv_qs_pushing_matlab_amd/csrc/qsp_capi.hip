@@ -54,7 +54,7 @@ struct qsp_solver {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int n_shapes = 0;
-    DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, qp_capped, cost;
+    DevBuf shapes, shape_id, x0, yref, yref_e, X, U, PI, Xo, Uo, PIo, u0, status, sqp_iter, qp_iter, qp_capped, qp_stalled, cost;
     DevBuf warm_valid, traj, index_time;
     // delay compensation (set_delay_comp, NMPC_controller.m:106-110): delay_buff_comp columns and the
     // per-lane controller input buffer u_buff_contr (B x D x 2, column 0 newest); closed-loop state
@@ -132,6 +132,7 @@ static void fill_params(qsp_solver* s) {
     p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
     p.qp_stall_iters = s->o.qp_stall_iters;
     p.qp_stall_alpha = s->o.qp_stall_alpha;
+    p.qp_mu_max = s->o.qp_mu_max;
     p.tol_stat = s->o.tol_stat;
     p.tol_eq = s->o.tol_eq;
     p.tol_ineq = s->o.tol_ineq;
@@ -210,6 +211,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.sqp_iter = s->sqp_iter.as<int32_t>();
     a.qp_iter = s->qp_iter.as<int32_t>();
     a.qp_capped = s->qp_capped.as<int32_t>();
+    a.qp_stalled = s->qp_stalled.as<int32_t>();
     a.cost = s->cost.as<double>();
     a.wX = s->wX.as<double>();
     a.wU = s->wU.as<double>();
@@ -325,6 +327,8 @@ void qsp_default_options(qsp_options* o) {
     o->stage0_s_bound = 1;          // acados: bgh constraints on stages 0..N-1
     o->qp_stall_iters = 3;          // stall exit: alpha < 1e-3 three times in a row
     o->qp_stall_alpha = 1e-3;
+    o->qp_mu_max = 1e100;           // divergence exit: overflow guard
+    o->struct_size = (int32_t)sizeof(qsp_options);
     // nlp_mode 1: NMPC_controller.m:275-276 tolerances; acados merit_backtracking defaults
     o->tol_stat = o->tol_eq = o->tol_ineq = o->tol_comp = 1e-6;
     o->ls_alpha_min = 0.05;
@@ -332,12 +336,16 @@ void qsp_default_options(qsp_options* o) {
     o->ls_eps = 1e-4;
 }
 
-int qsp_version(void) { return 1; }
+int qsp_version(void) { return QSP_ABI_VERSION; }
 
 const char* qsp_last_error(void) { return g_err.c_str(); }
 
 int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (!o || !out) return fail(QSP_ERR_ARG, "qsp_create: null argument");
+    if (o->struct_size != (int32_t)sizeof(qsp_options))
+        return fail(QSP_ERR_ARG, "qsp_create: qsp_options.struct_size != sizeof(qsp_options) (caller built "
+                                 "against another qsp_nmpc.h? check qsp_version() == QSP_ABI_VERSION)");
+    if (!(o->qp_mu_max > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: qp_mu_max must be > 0");
     if (o->N < 1 || o->batch < 1) return fail(QSP_ERR_ARG, "qsp_create: N and batch must be >= 1");
     if (o->nlp_mode != QSP_NLP_SQP_RTI_FIXED && o->nlp_mode != QSP_NLP_SQP_MERIT)
         return fail(QSP_ERR_ARG, "qsp_create: unsupported nlp_mode");
@@ -400,6 +408,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     al(s->sqp_iter, B * 4);
     al(s->qp_iter, B * 4);
     al(s->qp_capped, B * 4);
+    al(s->qp_stalled, B * 4);
     al(s->cost, B * 8);
     al(s->warm_valid, B);
     al(s->wX, B * (N + 1) * 4 * 8);
@@ -451,7 +460,7 @@ int qsp_destroy(qsp_solver* s) {
     (void)hipSetDevice(s->o.device);
     DevBuf* bufs[] = {&s->ubc, &s->ubp, &s->cl_x, &s->cl_xsim, &s->cl_amp,
                       &s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
-                      &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->qp_capped, &s->cost,
+                      &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->qp_capped, &s->qp_stalled, &s->cost,
                       &s->warm_valid,
                       &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
                       &s->whist};
@@ -518,6 +527,7 @@ int qsp_shape_from_ply(const char* path, int32_t flip, double mu_sg, double mu_s
     }
     std::memset(out, 0, sizeof(*out));
     out->n_ctrl = n;
+    out->struct_size = (int32_t)sizeof(qsp_shape);
     for (int i = 0; i < n; ++i) { out->ctrl[i][0] = srt[2 * i]; out->ctrl[i][1] = srt[2 * i + 1]; }
     // knots (getSpline :117-123): p = 3, m = n - 2, S = [0 0 0 linspace(0,b,m) b b b]
     double b = 0.0;
@@ -541,6 +551,8 @@ int qsp_set_shapes(qsp_solver* s, const qsp_shape* shapes, int32_t n) {
     std::vector<ShapeDev> h((size_t)n);
     for (int q = 0; q < n; ++q) {
         const qsp_shape& in = shapes[q];
+        if (in.struct_size != (int32_t)sizeof(qsp_shape))
+            return fail(QSP_ERR_ARG, "qsp_set_shapes: qsp_shape.struct_size != sizeof(qsp_shape) (stale layout?)");
         ShapeDev& d = h[q];
         std::memset(&d, 0, sizeof d);
         const int nc = in.n_ctrl;
@@ -672,6 +684,11 @@ int qsp_get_qp_iter(qsp_solver* s, int32_t* it) {
 int qsp_get_qp_capped(qsp_solver* s, int32_t* c) {
     if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_qp_capped: null argument");
     return d2h(s, c, s->qp_capped, (size_t)s->o.batch * 4);
+}
+
+int qsp_get_qp_stalled(qsp_solver* s, int32_t* c) {
+    if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_qp_stalled: null argument");
+    return d2h(s, c, s->qp_stalled, (size_t)s->o.batch * 4);
 }
 int qsp_get_time_tot(qsp_solver* s, double* ms) {
     if (!s || !ms) return fail(QSP_ERR_ARG, "qsp_get_time_tot: null argument");
@@ -925,9 +942,10 @@ int qsp_closed_loop_ex(qsp_solver* s, const qsp_closed_loop_opts* o, const doubl
         HIPCHK(hipMemcpyAsync(s->cl_amp.p, o->amplitude, B * 8, hipMemcpyHostToDevice, s->stream));
     }
     // initial_condition_update -> clear_variables: the first solve is a cold start (main.m:79);
-    // both input buffers start at zero (set_delay_comp / closed_loop_matlab's u_buff_plant)
+    // the plant's buffer starts at zero (closed_loop_matlab's u_buff_plant, helper.m:211-212); the
+    // controller's u_buff_contr is left as it is: the reference zeroes it only in set_delay_comp
+    // (NMPC_controller.m:106-110; qsp_set_delay_comp), so a second run continues from the first's
     HIPCHK(hipMemsetAsync(s->warm_valid.p, 0, B, s->stream));
-    if (s->D > 0) HIPCHK(hipMemsetAsync(s->ubc.p, 0, B * (size_t)s->D * 2 * 8, s->stream));
     if (Dp > 0) HIPCHK(hipMemsetAsync(s->ubp.p, 0, B * (size_t)Dp * 2 * 8, s->stream));
     ClosedLoopArgs c = cl_args(s);
     c.n_steps = n_steps;

@@ -37,6 +37,7 @@ struct SolveArgs {
     int32_t* sqp_iter;         // B
     int32_t* qp_iter;          // B (sum of IPM iterations)
     int32_t* qp_capped;        // B (QPs stopped by the iteration cap; nullptr: not counted)
+    int32_t* qp_stalled;       // B (QPs stopped by the stall exit; nullptr: not counted)
     double* cost;              // B
     // workspace (device, owned by the handle)
     double* wX;                // B x (N+1) x 4   SQP iterate

@@ -117,16 +117,8 @@ __device__ __forceinline__ double group_sum(double v, const GroupScan& g) {
 __device__ __forceinline__ double group_min(double v, const GroupScan& g) { return group_reduce(v, g, OpMin()); }
 __device__ __forceinline__ double group_max(double v, const GroupScan& g) { return group_reduce(v, g, OpMax()); }
 
-// 1/x from the hardware reciprocal refined by two Newton steps (≈ 5 instructions
-// instead of the ≈ 10 of the IEEE division sequence); for the positive, finite
-// arguments it is used on (slacks, a 2x2 determinant) it agrees with 1.0/x to an ulp.
-__device__ __forceinline__ double rcp(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-x, r, 1.0);
-    return fma(r, e, r);
-}
+// rcp(x): 1/x from the hardware reciprocal and two Newton steps (qsp_fp.hpp; ≈ 5 instructions
+// instead of the ≈ 10 of the IEEE division sequence, and the correctly rounded 1/x)
 
 // symmetric 4x4 stored as 10 entries: (0,0)(0,1)(0,2)(0,3)(1,1)(1,2)(1,3)(2,2)(2,3)(3,3)
 __device__ __forceinline__ int sidx(int i, int j) {
@@ -261,8 +253,7 @@ __device__ __forceinline__ void ric_terminal(const SolveParams& p, const double 
 
 // One backward factorisation step exploiting A = [[1,0,a0,a1],[0,1,a2,a3],[0,0,1,a4],[0,0,0,a5]].
 // Hx, Hu: diagonal stage Hessian (incl. barrier); gx, gu: gradient (incl. barrier).
-// Every sum is written as one left-to-right chain starting from its additive term, so
-// each product contracts into an FMA (no separate multiply + add per sum).
+// Every sum is one left-to-right FMA chain from its additive term (or its first product).
 __device__ __forceinline__ void ric_factor_step(const double a[6], const double B[8], const double bb[4],
                                                 const double Hx[4], const double Hu[2],
                                                 const double gx[4], const double gu[2],
@@ -280,8 +271,8 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     for (int i = 0; i < 4; ++i) {
         PA[i][0] = Pm[i][0];
         PA[i][1] = Pm[i][1];
-        PA[i][2] = Pm[i][2] + Pm[i][0] * a[0] + Pm[i][1] * a[2];
-        PA[i][3] = Pm[i][0] * a[1] + Pm[i][1] * a[3] + Pm[i][2] * a[4] + Pm[i][3] * a[5];
+        PA[i][2] = qfma(Pm[i][1], a[2], qfma(Pm[i][0], a[0], Pm[i][2]));
+        PA[i][3] = qfma(Pm[i][3], a[5], qfma(Pm[i][2], a[4], qfma(Pm[i][1], a[3], Pm[i][0] * a[1])));
     }
     // PB
     double PB[4][2];
@@ -289,27 +280,29 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-            PB[i][j] = Pm[i][0] * B[j] + Pm[i][1] * B[2 + j] + Pm[i][2] * B[4 + j] + Pm[i][3] * B[6 + j];
+            PB[i][j] = qfma(Pm[i][3], B[6 + j], qfma(Pm[i][2], B[4 + j], qfma(Pm[i][1], B[2 + j], Pm[i][0] * B[j])));
     // pp = p + P b
     double pp[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pp[i] = pv[i] + Pm[i][0] * bb[0] + Pm[i][1] * bb[1] + Pm[i][2] * bb[2] + Pm[i][3] * bb[3];
+    for (int i = 0; i < 4; ++i)
+        pp[i] = qfma(Pm[i][3], bb[3], qfma(Pm[i][2], bb[2], qfma(Pm[i][1], bb[1], qfma(Pm[i][0], bb[0], pv[i]))));
     // R~ = Hu + B'PB (sym), S~ = B'PA (2x4), r~ = gu + B'pp
-    const double R00 = Hu[0] + B[0] * PB[0][0] + B[2] * PB[1][0] + B[4] * PB[2][0] + B[6] * PB[3][0];
-    const double R01 = B[0] * PB[0][1] + B[2] * PB[1][1] + B[4] * PB[2][1] + B[6] * PB[3][1];
-    const double R11 = Hu[1] + B[1] * PB[0][1] + B[3] * PB[1][1] + B[5] * PB[2][1] + B[7] * PB[3][1];
+    const double R00 = qfma(B[6], PB[3][0], qfma(B[4], PB[2][0], qfma(B[2], PB[1][0], qfma(B[0], PB[0][0], Hu[0]))));
+    const double R01 = qfma(B[6], PB[3][1], qfma(B[4], PB[2][1], qfma(B[2], PB[1][1], B[0] * PB[0][1])));
+    const double R11 = qfma(B[7], PB[3][1], qfma(B[5], PB[2][1], qfma(B[3], PB[1][1], qfma(B[1], PB[0][1], Hu[1]))));
     // S~ = B'PA = (PB)'A with the structure of A
     double St[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         St[i][0] = PB[0][i];
         St[i][1] = PB[1][i];
-        St[i][2] = PB[2][i] + PB[0][i] * a[0] + PB[1][i] * a[2];
-        St[i][3] = PB[0][i] * a[1] + PB[1][i] * a[3] + PB[2][i] * a[4] + PB[3][i] * a[5];
+        St[i][2] = qfma(PB[1][i], a[2], qfma(PB[0][i], a[0], PB[2][i]));
+        St[i][3] = qfma(PB[3][i], a[5], qfma(PB[2][i], a[4], qfma(PB[1][i], a[3], PB[0][i] * a[1])));
     }
     double rt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rt[i] = gu[i] + B[i] * pp[0] + B[2 + i] * pp[1] + B[4 + i] * pp[2] + B[6 + i] * pp[3];
+    for (int i = 0; i < 2; ++i)
+        rt[i] = qfma(B[6 + i], pp[3], qfma(B[4 + i], pp[2], qfma(B[2 + i], pp[1], qfma(B[i], pp[0], gu[i]))));
     // Q~ = Hx + A'PA  (upper triangle), q~ = gx + A'pp
     double Qt[10];
 #pragma unroll
@@ -317,34 +310,34 @@ __device__ __forceinline__ void ric_factor_step(const double a[6], const double 
         const double c0 = PA[0][j], c1 = PA[1][j], c2 = PA[2][j], c3 = PA[3][j];
         if (j >= 0) Qt[sidx(0, j)] = c0;
         if (j >= 1) Qt[sidx(1, j)] = c1;
-        if (j >= 2) Qt[sidx(2, j)] = (j == 2 ? Hx[2] + c2 : c2) + a[0] * c0 + a[2] * c1;
-        if (j >= 3) Qt[sidx(3, j)] = Hx[3] + a[1] * c0 + a[3] * c1 + a[4] * c2 + a[5] * c3;
+        if (j >= 2) Qt[sidx(2, j)] = qfma(a[2], c1, qfma(a[0], c0, j == 2 ? Hx[2] + c2 : c2));
+        if (j >= 3) Qt[sidx(3, j)] = qfma(a[5], c3, qfma(a[4], c2, qfma(a[3], c1, qfma(a[1], c0, Hx[3]))));
     }
     Qt[0] += Hx[0]; Qt[4] += Hx[1];
     double qt[4];
     qt[0] = gx[0] + pp[0];
     qt[1] = gx[1] + pp[1];
-    qt[2] = gx[2] + pp[2] + a[0] * pp[0] + a[2] * pp[1];
-    qt[3] = gx[3] + a[1] * pp[0] + a[3] * pp[1] + a[4] * pp[2] + a[5] * pp[3];
+    qt[2] = qfma(a[2], pp[1], qfma(a[0], pp[0], gx[2] + pp[2]));
+    qt[3] = qfma(a[5], pp[3], qfma(a[4], pp[2], qfma(a[3], pp[1], qfma(a[1], pp[0], gx[3]))));
     // Rn = -R~^-1 (kept negated: the sign folds into the multiplies)
-    const double idet = rcp(R00 * R11 - R01 * R01);
+    const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
     Rn[0] = (-R11) * idet; Rn[1] = R01 * idet; Rn[2] = (-R00) * idet;
     // K = -R~^-1 S~ ; kk = -R~^-1 r~
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        K[j] = Rn[0] * St[0][j] + Rn[1] * St[1][j];
-        K[4 + j] = Rn[1] * St[0][j] + Rn[2] * St[1][j];
+        K[j] = qfma(Rn[1], St[1][j], Rn[0] * St[0][j]);
+        K[4 + j] = qfma(Rn[2], St[1][j], Rn[1] * St[0][j]);
     }
-    kk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
-    kk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
+    kk[0] = qfma(Rn[1], rt[1], Rn[0] * rt[0]);
+    kk[1] = qfma(Rn[2], rt[1], Rn[1] * rt[0]);
     // P = Q~ + S~'K ; p = q~ + K'r~ (not at stage 0: nothing reads P_0, p_0; upd is uniform)
     if (!upd) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = i; j < 4; ++j) P[sidx(i, j)] = Qt[sidx(i, j)] + St[0][i] * K[j] + St[1][i] * K[4 + j];
+        for (int j = i; j < 4; ++j) P[sidx(i, j)] = qfma(St[1][i], K[4 + j], qfma(St[0][i], K[j], Qt[sidx(i, j)]));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
+    for (int i = 0; i < 4; ++i) pv[i] = qfma(K[4 + i], rt[1], qfma(K[i], rt[0], qt[i]));
 }
 
 // Vector-only backward step of the Mehrotra corrector, on the DIFFERENCE to the predictor:
@@ -356,25 +349,26 @@ __device__ __forceinline__ void ric_delta_step(const double a[6], const double B
                                                const double K[8], const double Rn[3], double pv[4], double dkk[2]) {
     double rt[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rt[i] = dgu[i] + B[i] * pv[0] + B[2 + i] * pv[1] + B[4 + i] * pv[2] + B[6 + i] * pv[3];
+    for (int i = 0; i < 2; ++i)
+        rt[i] = qfma(B[6 + i], pv[3], qfma(B[4 + i], pv[2], qfma(B[2 + i], pv[1], qfma(B[i], pv[0], dgu[i]))));
     double qt[4];
     qt[0] = pv[0];
     qt[1] = pv[1];
-    qt[2] = pv[2] + a[0] * pv[0] + a[2] * pv[1];
-    qt[3] = dgx3 + a[1] * pv[0] + a[3] * pv[1] + a[4] * pv[2] + a[5] * pv[3];
-    dkk[0] = Rn[0] * rt[0] + Rn[1] * rt[1];
-    dkk[1] = Rn[1] * rt[0] + Rn[2] * rt[1];
+    qt[2] = qfma(a[2], pv[1], qfma(a[0], pv[0], pv[2]));
+    qt[3] = qfma(a[5], pv[3], qfma(a[4], pv[2], qfma(a[3], pv[1], qfma(a[1], pv[0], dgx3))));
+    dkk[0] = qfma(Rn[1], rt[1], Rn[0] * rt[0]);
+    dkk[1] = qfma(Rn[2], rt[1], Rn[1] * rt[0]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pv[i] = qt[i] + K[i] * rt[0] + K[4 + i] * rt[1];
+    for (int i = 0; i < 4; ++i) pv[i] = qfma(K[4 + i], rt[1], qfma(K[i], rt[0], qt[i]));
 }
 
 // dx_{k+1} = A dx + B du + b
 __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], const double bb[4],
                                          const double du[2], double dx[4]) {
-    const double n0 = bb[0] + dx[0] + a[0] * dx[2] + a[1] * dx[3] + B[0] * du[0] + B[1] * du[1];
-    const double n1 = bb[1] + dx[1] + a[2] * dx[2] + a[3] * dx[3] + B[2] * du[0] + B[3] * du[1];
-    const double n2 = bb[2] + dx[2] + a[4] * dx[3] + B[4] * du[0] + B[5] * du[1];
-    const double n3 = bb[3] + a[5] * dx[3] + B[6] * du[0] + B[7] * du[1];
+    const double n0 = qfma(B[1], du[1], qfma(B[0], du[0], qfma(a[1], dx[3], qfma(a[0], dx[2], bb[0] + dx[0]))));
+    const double n1 = qfma(B[3], du[1], qfma(B[2], du[0], qfma(a[3], dx[3], qfma(a[2], dx[2], bb[1] + dx[1]))));
+    const double n2 = qfma(B[5], du[1], qfma(B[4], du[0], qfma(a[4], dx[3], bb[2] + dx[2])));
+    const double n3 = qfma(B[7], du[1], qfma(B[6], du[0], qfma(a[5], dx[3], bb[3])));
     dx[0] = n0; dx[1] = n1; dx[2] = n2; dx[3] = n3;
 }
 
@@ -391,7 +385,7 @@ __device__ __forceinline__ void barrier_terms(const Ctx& c, const SolveParams& p
         const bool act = bnd_act(c, p, k, j);
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double sl = ll * st.rt(ls, 2 * j), sh = lh * st.rt(ls, 2 * j + 1);
-        const double gadd = (-sl * lo[j] - sh * hi[j]) + (lh - ll);
+        const double gadd = qfma(-sh, hi[j], -sl * lo[j]) + (lh - ll);
         st.hg(ls, j) = act ? sl + sh : 0.0;
         st.hg(ls, 3 + j) = act ? gadd : 0.0;
     }
@@ -419,8 +413,8 @@ __device__ __forceinline__ void affine_dirs(const Ctx& c, const SolveParams& p, 
         const double v = st.f(F_VA, ls, j);
         at[2 * j] = v - lo[j] - tl;
         at[2 * j + 1] = hi[j] - v - th;
-        al[2 * j] = -ll - sl * at[2 * j];
-        al[2 * j + 1] = -lh - sh * at[2 * j + 1];
+        al[2 * j] = qfma(-sl, at[2 * j], -ll);
+        al[2 * j + 1] = qfma(-sh, at[2 * j + 1], -lh);
         const double dtl = act ? at[2 * j] : 0.0, dth = act ? at[2 * j + 1] : 0.0;
         const double dll = act ? al[2 * j] : 0.0, dlh = act ? al[2 * j + 1] : 0.0;
         if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
@@ -434,9 +428,8 @@ __device__ __forceinline__ void affine_dirs(const Ctx& c, const SolveParams& p, 
 template <int S>
 __device__ __forceinline__ double affine_mu_part(const Ctx& c, const SolveParams& p, const Stage<S>& st, int ls,
                                                  const double at[6],
-                                                 const double al[6], double aa) {
+                                                 const double al[6], double aa, double part) {
     const int k = kof<S>(c, ls);
-    double part = 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const bool act = bnd_act(c, p, k, j);
@@ -444,7 +437,8 @@ __device__ __forceinline__ double affine_mu_part(const Ctx& c, const SolveParams
         const double ll = st.lm(ls, 2 * j), lh = st.lm(ls, 2 * j + 1);
         const double dtl = act ? at[2 * j] : 0.0, dth = act ? at[2 * j + 1] : 0.0;
         const double dll = act ? al[2 * j] : 0.0, dlh = act ? al[2 * j + 1] : 0.0;
-        part += (tl + aa * dtl) * (ll + aa * dll) + (th + aa * dth) * (lh + aa * dlh);
+        part = qfma(qfma(aa, dtl, tl), qfma(aa, dll, ll), part);
+        part = qfma(qfma(aa, dth, th), qfma(aa, dlh, lh), part);
     }
     return part;
 }
@@ -459,8 +453,8 @@ __device__ __forceinline__ void corrector_terms(const Ctx& c, const SolveParams&
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const bool act = bnd_act(c, p, k, j);
-        const double cl = smu - at[2 * j] * al[2 * j], ch = smu - at[2 * j + 1] * al[2 * j + 1];
-        st.hg(ls, 3 + j) = act ? ch * st.rt(ls, 2 * j + 1) - cl * st.rt(ls, 2 * j) : 0.0;
+        const double cl = qfma(-at[2 * j], al[2 * j], smu), ch = qfma(-at[2 * j + 1], al[2 * j + 1], smu);
+        st.hg(ls, 3 + j) = act ? qfma(ch, st.rt(ls, 2 * j + 1), -(cl * st.rt(ls, 2 * j))) : 0.0;
     }
 }
 
@@ -482,9 +476,9 @@ __device__ __forceinline__ void corrector_dirs(const Ctx& c, const SolveParams& 
         const double sl = ll * rtl, sh = lh * rth;
         const double v = st.f(F_VN, ls, j);
         double dtl = v - lo[j] - tl, dth = hi[j] - v - th;
-        double dll = -ll - sl * dtl, dlh = -lh - sh * dth;
-        dll += (smu - at[2 * j] * al[2 * j]) * rtl;
-        dlh += (smu - at[2 * j + 1] * al[2 * j + 1]) * rth;
+        double dll = qfma(-sl, dtl, -ll), dlh = qfma(-sh, dth, -lh);
+        dll = qfma(qfma(-at[2 * j], al[2 * j], smu), rtl, dll);
+        dlh = qfma(qfma(-at[2 * j + 1], al[2 * j + 1], smu), rth, dlh);
         dtl = act ? dtl : 0.0; dth = act ? dth : 0.0;
         dll = act ? dll : 0.0; dlh = act ? dlh : 0.0;
         if (dtl < 0.0 && tl * den < num * -dtl) { num = tl; den = -dtl; }
@@ -502,10 +496,10 @@ __device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const dou
                                            double alpha) {
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-        const double tn = st.t(ls, q) + alpha * dt[q];
+        const double tn = qfma(alpha, dt[q], st.t(ls, q));
         st.t(ls, q) = tn;
         st.rt(ls, q) = rcp(tn);
-        st.lm(ls, q) = st.lm(ls, q) + alpha * dl[q];
+        st.lm(ls, q) = qfma(alpha, dl[q], st.lm(ls, q));
     }
 }
 
@@ -536,9 +530,9 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 #pragma unroll
     for (int ls = 0; ls < S; ++ls) {
         if (FACTOR) {
-            hx3[ls] = p.tau * p.W[3] + st.hg(ls, 0);
-            hu[ls][0] = p.tau * p.W[4] + st.hg(ls, 1);
-            hu[ls][1] = p.tau * p.W[5] + st.hg(ls, 2);
+            hx3[ls] = qfma(p.tau, p.W[3], st.hg(ls, 0));
+            hu[ls][0] = qfma(p.tau, p.W[4], st.hg(ls, 1));
+            hu[ls][1] = qfma(p.tau, p.W[5], st.hg(ls, 2));
             gx3[ls] = st.g[ls][3] + st.hg(ls, 3);
             gu[ls][0] = st.g[ls][4] + st.hg(ls, 4);
             gu[ls][1] = st.g[ls][5] + st.hg(ls, 5);
@@ -556,7 +550,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         const double* K = st.K[0];
         double e[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) e[i] = (i == 3 ? gx3[0] : 0.0) + K[i] * gu[0][0] + K[4 + i] * gu[0][1];
+        for (int i = 0; i < 4; ++i) e[i] = qfma(K[4 + i], gu[0][1], qfma(K[i], gu[0][0], i == 3 ? gx3[0] : 0.0));
         // Step j runs on lanes lig <= j only: lane j-1 takes lane j's value, while lane j,
         // whose source lane j+1 sits the step out, keeps its old value (a DPP read from a
         // disabled lane returns `old`) — so every lane ends holding the dp that reached it.
@@ -566,7 +560,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 double n[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    n[i] = e[i] + M[0][i] * pv[0] + M[0][4 + i] * pv[1] + M[0][8 + i] * pv[2] + M[0][12 + i] * pv[3];
+                    n[i] = qfma(M[0][12 + i], pv[3], qfma(M[0][8 + i], pv[2], qfma(M[0][4 + i], pv[1], qfma(M[0][i], pv[0], e[i]))));
 #pragma unroll
                 for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], n[i]);
             }
@@ -578,9 +572,9 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             double rt[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-                rt[i] = gu[0][i] + B[i] * dpk[0] + B[2 + i] * dpk[1] + B[4 + i] * dpk[2] + B[6 + i] * dpk[3];
-            st.kk[0][0] += Rn[0] * rt[0] + Rn[1] * rt[1];
-            st.kk[0][1] += Rn[1] * rt[0] + Rn[2] * rt[1];
+                rt[i] = qfma(B[6 + i], dpk[3], qfma(B[4 + i], dpk[2], qfma(B[2 + i], dpk[1], qfma(B[i], dpk[0], gu[0][i]))));
+            st.kk[0][0] = qfma(Rn[1], rt[1], qfma(Rn[0], rt[0], st.kk[0][0]));
+            st.kk[0][1] = qfma(Rn[2], rt[1], qfma(Rn[1], rt[0], st.kk[0][1]));
         }
     } else
     for (int j = c.L - 1; j >= 0; --j) {
@@ -639,11 +633,11 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) M[0][4 * i + q] = Am[i][q] + B[2 * i] * K[q] + B[2 * i + 1] * K[4 + q];
+                for (int q = 0; q < 4; ++q) M[0][4 * i + q] = qfma(B[2 * i + 1], K[4 + q], qfma(B[2 * i], K[q], Am[i][q]));
         }
         double cv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cv[i] = st.bb[0][i] + st.B[0][2 * i] * st.kk[0][0] + st.B[0][2 * i + 1] * st.kk[0][1];
+        for (int i = 0; i < 4; ++i) cv[i] = qfma(st.B[0][2 * i + 1], st.kk[0][1], qfma(st.B[0][2 * i], st.kk[0][0], st.bb[0][i]));
         double dx[4] = {dx0[0], dx0[1], dx0[2], dx0[3]};
         // Step j runs on lanes j <= lig < L-1 only (the terminal lane never steps, so the
         // next group's first lane reads a disabled source): lane j+1 takes lane j's value and
@@ -653,8 +647,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 double n[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    n[i] = cv[i] + M[0][4 * i] * dx[0] + M[0][4 * i + 1] * dx[1] + M[0][4 * i + 2] * dx[2] +
-                           M[0][4 * i + 3] * dx[3];
+                    n[i] = qfma(M[0][4 * i + 3], dx[3], qfma(M[0][4 * i + 2], dx[2], qfma(M[0][4 * i + 1], dx[1], qfma(M[0][4 * i], dx[0], cv[i]))));
 #pragma unroll
                 for (int i = 0; i < 4; ++i) dx[i] = wave_from_prev(dx[i], n[i]);
             }
@@ -663,8 +656,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         if (c.lig < c.N) {
             const double* K = st.K[0];
             st.f(out, 0, 0) = dxk[3];
-            st.f(out, 0, 1) = st.kk[0][0] + K[0] * dxk[0] + K[1] * dxk[1] + K[2] * dxk[2] + K[3] * dxk[3];
-            st.f(out, 0, 2) = st.kk[0][1] + K[4] * dxk[0] + K[5] * dxk[1] + K[6] * dxk[2] + K[7] * dxk[3];
+            st.f(out, 0, 1) = qfma(K[3], dxk[3], qfma(K[2], dxk[2], qfma(K[1], dxk[1], qfma(K[0], dxk[0], st.kk[0][0]))));
+            st.f(out, 0, 2) = qfma(K[7], dxk[3], qfma(K[6], dxk[2], qfma(K[5], dxk[1], qfma(K[4], dxk[0], st.kk[0][1]))));
         }
         return;
     }
@@ -676,8 +669,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         for (int ls = 0; ls < S; ++ls) {
             if (j == c.L - 1 && ls >= lsN) continue;
             double du[2];
-            du[0] = st.kk[ls][0] + st.K[ls][0] * dx[0] + st.K[ls][1] * dx[1] + st.K[ls][2] * dx[2] + st.K[ls][3] * dx[3];
-            du[1] = st.kk[ls][1] + st.K[ls][4] * dx[0] + st.K[ls][5] * dx[1] + st.K[ls][6] * dx[2] + st.K[ls][7] * dx[3];
+            du[0] = qfma(st.K[ls][3], dx[3], qfma(st.K[ls][2], dx[2], qfma(st.K[ls][1], dx[1], qfma(st.K[ls][0], dx[0], st.kk[ls][0]))));
+            du[1] = qfma(st.K[ls][7], dx[3], qfma(st.K[ls][6], dx[2], qfma(st.K[ls][5], dx[1], qfma(st.K[ls][4], dx[0], st.kk[ls][1]))));
             if (act) {
                 st.f(out, ls, 0) = dx[3];
                 st.f(out, ls, 1) = du[0];
@@ -690,10 +683,19 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
     }
 }
 
+enum QpExit : int { QP_EXIT_CONV = 0, QP_EXIT_CAP = 1, QP_EXIT_STALL = 2, QP_EXIT_DIVERGED = 3 };
+
 // Mehrotra predictor-corrector IPM on the current linearisation.  Leaves the
 // damped control step in LDS (F_DU) and the slacks/multipliers in F_T / F_LM.
-// Returns the number of iterations taken by this lane's instance; `conv` tells whether the
-// stop test was met (false: the iteration cap stopped it, as HPIPM at iter_max).
+// Returns the number of iterations taken by this lane's instance and, in `exit`, why it stopped
+// (group-uniform): QP_EXIT_CONV the stop test was met; QP_EXIT_CAP the iteration cap (its last
+// iterate is used, as HPIPM's at iter_max); QP_EXIT_STALL the step length stayed below
+// qp_stall_alpha for qp_stall_iters iterations (locally infeasible linearisation, HPIPM's
+// min-step exit; the last iterate is used as at the cap); QP_EXIT_DIVERGED mu left
+// [0, qp_mu_max) (multipliers growing without bound, or non-finite): a QP failure (acados
+// ACADOS_QP_FAILURE, status 4), stopped while its iterate is still finite.  A stopped instance's
+// state is frozen while the rest of its wave iterates (no update with alpha = 0, which would turn
+// an infinite direction into NaN).
 //
 // Stop test (HPIPM's four exit residuals, ocp_qp_ipm): complementarity mu < mu_stop, bound
 // residual < res_stop, stationarity < qp_tol_stat, equality < qp_tol_eq.  The three linear
@@ -703,7 +705,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
 // r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)); the
 // test r * prod < tol is applied as prod < min(tol / r) over the three.
 template <int S>
-__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], bool& conv,
+__device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], int& exit,
                       bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
     // initial point.  r0 = largest bound residual of the infeasible start (t - d where the
@@ -727,7 +729,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
             st.rt(ls, 2 * j + 1) = act ? rh : 1.0;
             st.lm(ls, 2 * j) = act ? p.mu0 * rl : 0.0;
             st.lm(ls, 2 * j + 1) = act ? p.mu0 * rh : 0.0;
-            gl[j] = act ? p.mu0 * rh - p.mu0 * rl : 0.0;
+            gl[j] = act ? qfma(p.mu0, rh, -(p.mu0 * rl)) : 0.0;
         }
         // start-point stationarity g + C' lam (bounded components s, u_n, u_t) and equality
         // (defects; x0 on the first stage); the padding slots past the terminal stage hold zeros
@@ -755,17 +757,21 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
     rs_stop = rs_b < rs_stop ? rs_b : rs_stop;
     double rscale = 1.0;
     int nit = 0, stall = 0;
+    bool conv = false, stalled = false, div = false;
     for (int it = 0;; ++it) {
         double tl_sum = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls)
 #pragma unroll
-            for (int q = 0; q < 6; ++q) tl_sum += st.t(ls, q) * st.lm(ls, q);
+            for (int q = 0; q < 6; ++q) tl_sum = qfma(st.t(ls, q), st.lm(ls, q), tl_sum);
         const double mu = group_sum(tl_sum, c.gs) / m;
-        conv = skip || (!(mu >= p.mu_stop) && !(rscale >= rs_stop));
-        // stall exit (locally infeasible QP: the step length stays tiny while mu grows): stops
-        // like the cap, after the stop test had its chance
-        const bool done = conv || (p.qp_stall_iters > 0 && stall >= p.qp_stall_iters);
+        // divergence first (mu non-finite or past qp_mu_max: a NaN mu would pass the stop test),
+        // then the stop test, then the stall exit (locally infeasible QP: the step length stays
+        // tiny while mu grows)
+        div = !skip && !(mu < p.qp_mu_max);
+        conv = !div && (skip || (!(mu >= p.mu_stop) && !(rscale >= rs_stop)));
+        stalled = !conv && !div && p.qp_stall_iters > 0 && stall >= p.qp_stall_iters;
+        const bool done = conv || div || stalled;
         // the cap is tested after the last step too (conv reports it), then the loop ends
         if (it == p.qp_iters || __ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
@@ -782,7 +788,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         const double aa = group_min(num / den, c.gs);
         double ma = 0.0;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) ma += affine_mu_part<S>(c, p, st, ls, at[ls], al[ls], aa);
+        for (int ls = 0; ls < S; ++ls) ma = affine_mu_part<S>(c, p, st, ls, at[ls], al[ls], aa, ma);
         const double mua = group_sum(ma, c.gs) / m;
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
@@ -797,17 +803,19 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         for (int ls = 0; ls < S; ++ls) corrector_dirs<S>(c, p, st, ls, at[ls], al[ls], smu, dt[ls], dl[ls], num, den);
         double alpha = p.frac * group_min(num / den, c.gs);
         alpha = fmin(alpha, 1.0);
-        // (a finished instance keeps its count: it sits the rest of the wave's loop out at alpha = 0)
-        stall = done ? stall : (alpha < p.qp_stall_alpha ? stall + 1 : 0);
-        if (done) alpha = 0.0;
-        rscale *= 1.0 - alpha;
+        // a finished instance sits the rest of the wave's loop out with its state frozen
+        if (!done) {
+            stall = alpha < p.qp_stall_alpha ? stall + 1 : 0;
+            rscale *= 1.0 - alpha;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            apply_step<S>(st, ls, dt[ls], dl[ls], alpha);
-            st.du(ls, 0) += alpha * (st.f(F_VN, ls, 1) - st.du(ls, 0));
-            st.du(ls, 1) += alpha * (st.f(F_VN, ls, 2) - st.du(ls, 1));
+            for (int ls = 0; ls < S; ++ls) {
+                apply_step<S>(st, ls, dt[ls], dl[ls], alpha);
+                st.du(ls, 0) = qfma(alpha, st.f(F_VN, ls, 1) - st.du(ls, 0), st.du(ls, 0));
+                st.du(ls, 1) = qfma(alpha, st.f(F_VN, ls, 2) - st.du(ls, 1), st.du(ls, 1));
+            }
         }
     }
+    exit = conv ? QP_EXIT_CONV : (div ? QP_EXIT_DIVERGED : (stalled ? QP_EXIT_STALL : QP_EXIT_CAP));
     return nit;
 }
 
@@ -835,6 +843,19 @@ __device__ __forceinline__ void qp_rollout(const Ctx& c, Stage<S>& st, const dou
     }
 }
 
+// One step of the adjoint recursion  pi_{k-1} = Hx dx_k + gx_k + A_k' pi_k + (lam_hi - lam_lo)_s
+__device__ __forceinline__ void adjoint_step(const SolveParams& p, const double a[6], const double dx[4],
+                                             const double g[6], double dlam_s, double pi[4]) {
+    double np[4];
+    np[0] = qfma(p.tau * p.W[0], dx[0], g[0]) + pi[0];
+    np[1] = qfma(p.tau * p.W[1], dx[1], g[1]) + pi[1];
+    np[2] = qfma(p.tau * p.W[2], dx[2], g[2]) + (qfma(a[2], pi[1], a[0] * pi[0]) + pi[2]);
+    np[3] = qfma(p.tau * p.W[3], dx[3], g[3]) + qfma(a[5], pi[3], qfma(a[4], pi[2], qfma(a[3], pi[1], a[1] * pi[0])));
+    np[3] += dlam_s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pi[i] = np[i];
+}
+
 // Dynamics multipliers by the adjoint recursion; writes PI (B x N x 4).
 //   pi_{N-1} = We dx_N + g_N ; pi_{k-1} = Hx dx_k + gx_k + A_k' pi_k + (lam_hi - lam_lo)_s
 template <int S>
@@ -848,7 +869,7 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
                 const int k = j * S + ls;
                 if (k == c.N) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) pi[i] = p.We[i] * st.dxs(ls, i) + st.g[ls][i];
+                    for (int i = 0; i < 4; ++i) pi[i] = qfma(p.We[i], st.dxs(ls, i), st.g[ls][i]);
                 } else if (k < c.N) {
                     if (write && (!shift || k >= 1)) {
 #pragma unroll
@@ -859,16 +880,8 @@ __device__ __forceinline__ void qp_adjoint_store(const Ctx& c, const SolveParams
                         for (int i = 0; i < 4; ++i) PI[(size_t)k * 4 + i] = pi[i];
                     }
                     if (k >= 1) {
-                        const double* a = st.a[ls];
-                        double np[4];
-                        np[0] = p.tau * p.W[0] * st.dxs(ls, 0) + st.g[ls][0] + pi[0];
-                        np[1] = p.tau * p.W[1] * st.dxs(ls, 1) + st.g[ls][1] + pi[1];
-                        np[2] = p.tau * p.W[2] * st.dxs(ls, 2) + st.g[ls][2] + (a[0] * pi[0] + a[2] * pi[1] + pi[2]);
-                        np[3] = p.tau * p.W[3] * st.dxs(ls, 3) + st.g[ls][3] +
-                                (a[1] * pi[0] + a[3] * pi[1] + a[4] * pi[2] + a[5] * pi[3]);
-                        np[3] += st.lm(ls, 1) - st.lm(ls, 0);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) pi[i] = np[i];
+                        const double dxk[4] = {st.dxs(ls, 0), st.dxs(ls, 1), st.dxs(ls, 2), st.dxs(ls, 3)};
+                        adjoint_step(p, st.a[ls], dxk, st.g[ls], st.lm(ls, 1) - st.lm(ls, 0), pi);
                     }
                 }
             }
@@ -932,6 +945,7 @@ __global__ void prologue_kernel(SolveArgs A) {
     double* U = A.wU + (size_t)i * N * 2;
     A.qp_iter[i] = 0;
     if (A.qp_capped) A.qp_capped[i] = 0;
+    if (A.qp_stalled) A.qp_stalled[i] = 0;
     if (A.wdone) A.wdone[i] = 0;
     if (A.wnit) A.wnit[i] = 0;
     if (!(A.flags & QSP_FLAG_CONTROLLER)) {
@@ -942,7 +956,7 @@ __global__ void prologue_kernel(SolveArgs A) {
         s0_feasible(A, i, x0[3]);
         return;
     }
-    x0[3] = mat_mod(x0[3], sh.b) - sh.b * ((x0[3] < 0.0) ? 1.0 : 0.0);   // :332
+    x0[3] = qfma(-sh.b, (x0[3] < 0.0) ? 1.0 : 0.0, mat_mod(x0[3], sh.b));   // :332
     for (int c = 0; c < 4; ++c) A.wx0[(size_t)i * 4 + c] = x0[c];
     const bool cold = (A.warm_valid == nullptr || A.warm_valid[i] == 0);
     if (p.nlp_mode == 1) nlp_init(A, i, !cold);                             // :351-355 (PI = 0 cold)
@@ -963,7 +977,7 @@ __global__ void prologue_kernel(SolveArgs A) {
         }
         DynOut d;
         dynamics<false>(sh, xc[2], xc[3], U[2 * k], U[2 * k + 1], d);
-        for (int c = 0; c < 4; ++c) xc[c] = xc[c] + p.Ts * d.f[c];
+        for (int c = 0; c < 4; ++c) xc[c] = qfma(p.Ts, d.f[c], xc[c]);
     }
     s0_feasible(A, i, x0[3]);
 }
@@ -981,21 +995,13 @@ __device__ __forceinline__ void qp_adjoint_lane(const Ctx& c, const SolveParams&
         if (c.lig == j) {
             if (j == c.N) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) pi[i] = p.We[i] * st.dxs(0, i) + st.g[0][i];
+                for (int i = 0; i < 4; ++i) pi[i] = qfma(p.We[i], st.dxs(0, i), st.g[0][i]);
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) piq[i] = pi[i];
                 if (j >= 1) {
-                    const double* a = st.a[0];
-                    double np[4];
-                    np[0] = p.tau * p.W[0] * st.dxs(0, 0) + st.g[0][0] + pi[0];
-                    np[1] = p.tau * p.W[1] * st.dxs(0, 1) + st.g[0][1] + pi[1];
-                    np[2] = p.tau * p.W[2] * st.dxs(0, 2) + st.g[0][2] + (a[0] * pi[0] + a[2] * pi[1] + pi[2]);
-                    np[3] = p.tau * p.W[3] * st.dxs(0, 3) + st.g[0][3] +
-                            (a[1] * pi[0] + a[3] * pi[1] + a[4] * pi[2] + a[5] * pi[3]);
-                    np[3] += st.lm(0, 1) - st.lm(0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) pi[i] = np[i];
+                    const double dxk[4] = {st.dxs(0, 0), st.dxs(0, 1), st.dxs(0, 2), st.dxs(0, 3)};
+                    adjoint_step(p, st.a[0], dxk, st.g[0], st.lm(0, 1) - st.lm(0, 0), pi);
                 }
             }
         }
@@ -1012,24 +1018,24 @@ __device__ __forceinline__ double merit_stage(const SolveParams& p, int k, const
     if (k == p.N) {
         double s = 0.0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { const double r = x[i] - ye[i]; s += p.We[i] * r * r; }
+        for (int i = 0; i < 4; ++i) { const double r = x[i] - ye[i]; s = qfma(p.We[i] * r, r, s); }
         return 0.5 * s;
     }
     double s = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { const double r = x[i] - yr[i]; s += p.W[i] * r * r; }
+    for (int i = 0; i < 4; ++i) { const double r = x[i] - yr[i]; s = qfma(p.W[i] * r, r, s); }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) { const double r = u[i] - yr[4 + i]; s += p.W[4 + i] * r * r; }
+    for (int i = 0; i < 2; ++i) { const double r = u[i] - yr[4 + i]; s = qfma(p.W[4 + i] * r, r, s); }
     double ph = 0.5 * p.tau * s;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ph += nu[i] * fabs(def[i]);
+    for (int i = 0; i < 4; ++i) ph = qfma(nu[i], fabs(def[i]), ph);
     const double v[3] = {x[3], u[0], u[1]};
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         if (j == 0 && k == 0 && !p.s0_bound) continue;
         const double vl = p.lh[j] - v[j], vh = v[j] - p.uh[j];
-        if (vl > 0.0) ph += eta[2 * j] * vl;
-        if (vh > 0.0) ph += eta[2 * j + 1] * vh;
+        if (vl > 0.0) ph = qfma(eta[2 * j], vl, ph);
+        if (vh > 0.0) ph = qfma(eta[2 * j + 1], vh, ph);
     }
     return ph;
 }
@@ -1063,13 +1069,13 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
         const double* a = st.a[0];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const double r = st.g[0][4 + i] + (B[i] * PIk[0] + B[2 + i] * PIk[1] + B[4 + i] * PIk[2] + B[6 + i] * PIk[3]) +
+            const double r = (st.g[0][4 + i] + qfma(B[6 + i], PIk[3], qfma(B[4 + i], PIk[2], qfma(B[2 + i], PIk[1], B[i] * PIk[0])))) +
                              (LAMk[2 * (1 + i) + 1] - LAMk[2 * (1 + i)]);
             rs = fmax(rs, fabs(r));
         }
         if (k >= 1) {
-            const double at[4] = {PIk[0], PIk[1], a[0] * PIk[0] + a[2] * PIk[1] + PIk[2],
-                                  a[1] * PIk[0] + a[3] * PIk[1] + a[4] * PIk[2] + a[5] * PIk[3]};
+            const double at[4] = {PIk[0], PIk[1], qfma(a[2], PIk[1], a[0] * PIk[0]) + PIk[2],
+                                  qfma(a[5], PIk[3], qfma(a[4], PIk[2], qfma(a[3], PIk[1], a[1] * PIk[0])))};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 double r = st.g[0][i] - PIp[i] + at[i];
@@ -1096,6 +1102,36 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
     ri = group_max(ri, c.gs);
     rc = group_max(rc, c.gs);
     return rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
+}
+
+// The SQP's reaction to a QP's exit (both SQP kernels): counts of capped and stalled QPs; a
+// diverged QP (status 4, acados ACADOS_QP_FAILURE) or a non-finite solution (status 1) stops the
+// instance's SQP with its last iterate, as the oracle's sqp_solve does.  Returns that failure.
+template <int S>
+__device__ __forceinline__ bool qp_outcome(const SolveArgs& A, const Ctx& c, const Stage<S>& st, int iv, int it,
+                                           int exit, bool skip) {
+    const int N = c.N;
+    if (c.real && c.lig == 0 && !skip) {
+        if (A.qp_capped && exit == QP_EXIT_CAP) A.qp_capped[iv] += 1;
+        if (A.qp_stalled && exit == QP_EXIT_STALL) A.qp_stalled[iv] += 1;
+    }
+    if (!A.wdone) return false;
+    double bad = 0.0;
+#pragma unroll
+    for (int ls = 0; ls < S; ++ls) {
+        const int k = kof<S>(c, ls);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
+        bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
+    }
+    const double badg = group_max(bad, c.gs);   // every lane takes part in the DPP scan
+    const bool div = exit == QP_EXIT_DIVERGED;
+    const bool failed = !skip && (div || badg > 0.0);
+    if (failed && c.real && c.lig == 0) {
+        A.wdone[iv] = div ? 4 : 2;
+        A.sqp_iter[iv] = it;
+    }
+    return failed;
 }
 
 template <int S, bool MERIT = false, bool LIN = false>
@@ -1208,29 +1244,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             A.sqp_iter[iv] = it;
         }
     }
-    bool conv;
-    const int nit = qp_ipm<S>(c, p, st, dx0, conv, skip);
+    int exit;
+    const int nit = qp_ipm<S>(c, p, st, dx0, exit, skip);
     qp_rollout<S>(c, st, dx0);
-    // QPs stopped by the iteration cap (their last iterate is used, as HPIPM's at iter_max)
-    if (A.qp_capped && c.real && c.lig == 0 && !skip && !conv) A.qp_capped[iv] += 1;
-    // a non-finite QP solution stops the instance's SQP with its last iterate (status 1),
-    // as the oracle's sqp_solve does
-    bool failed = false;
-    if (A.wdone) {
-        double bad = 0.0;
-#pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            const int k = kof<S>(c, ls);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
-            bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
-        }
-        failed = !skip && group_max(bad, c.gs) > 0.0;
-        if (failed && c.real && c.lig == 0) {
-            A.wdone[iv] = 2;
-            A.sqp_iter[iv] = it;
-        }
-    }
+    const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
     if (A.wnit && c.real && c.lig == 0) {
         // wave-packing record and key of this instance for the next launch
         // (sort_by_iters_kernel); an instance that did not iterate keeps its record
@@ -1273,7 +1290,9 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
                 for (int q = 0; q < 6; ++q) A.qp_lam[((size_t)iv * N + k) * 6 + q] = st.lm(ls, q);
             }
             if (k == 0) A.qp_iter[iv] = nit;
-            if (k == 0 && A.qp_capped) A.qp_capped[iv] = conv ? 0 : 2;   // QP status: 0 stop test met, 2 cap
+            // QP status: 0 stop test met, 2 cap, 4 stall (min step), 5 diverged (qsp_qp_solve)
+            if (k == 0 && A.qp_capped)
+                A.qp_capped[iv] = exit == QP_EXIT_CONV ? 0 : (exit == QP_EXIT_CAP ? 2 : (exit == QP_EXIT_STALL ? 4 : 5));
         }
         return;
     }
@@ -1384,23 +1403,10 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
 #pragma unroll
         for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
         const bool skip = stopped || !c.real;
-        bool conv;
-        const int nit = qp_ipm<S>(c, p, st, dx0, conv, skip);
+        int exit;
+        const int nit = qp_ipm<S>(c, p, st, dx0, exit, skip);
         qp_rollout<S>(c, st, dx0);
-        if (A.qp_capped && c.real && c.lig == 0 && !skip && !conv) A.qp_capped[iv] += 1;
-        double bad = 0.0;
-#pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            const int k = kof<S>(c, ls);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bad = (k > N || isfinite(st.dxs(ls, q))) ? bad : 1.0;
-            bad = (k >= N || (isfinite(st.du(ls, 0)) && isfinite(st.du(ls, 1)))) ? bad : 1.0;
-        }
-        const bool failed = !skip && group_max(bad, c.gs) > 0.0;
-        if (failed && c.real && c.lig == 0) {
-            A.wdone[iv] = 2;
-            A.sqp_iter[iv] = it;
-        }
+        const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
         qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real && !skip && !failed,
                             (A.flags & QSP_FLAG_SHIFT) != 0);
         if (c.real && !skip && !failed) {
@@ -1561,18 +1567,18 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     const double* ye = A.yref_e + (size_t)iv * 4;
     double dph = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dph += g[i] * dxk[i];
+    for (int i = 0; i < 4; ++i) dph = qfma(g[i], dxk[i], dph);
     if (stg) {
-        dph += g[4] * duk[0] + g[5] * duk[1];
+        dph = qfma(g[5], duk[1], qfma(g[4], duk[0], dph));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dph -= NUk[i] * fabs(bb[i]);
+        for (int i = 0; i < 4; ++i) dph = qfma(-NUk[i], fabs(bb[i]), dph);
         const double v[3] = {xk[3], uk[0], uk[1]};
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             if (j == 0 && k == 0 && !p.s0_bound) continue;
             const double lo = p.lh[j] - v[j], hi = p.uh[j] - v[j];
-            if (lo > 0.0) dph -= ETAk[2 * j] * lo;
-            if (hi < 0.0) dph -= ETAk[2 * j + 1] * (-hi);
+            if (lo > 0.0) dph = qfma(-ETAk[2 * j], lo, dph);
+            if (hi < 0.0) dph = qfma(ETAk[2 * j + 1], hi, dph);
         }
     }
     const double phi0 = group_sum(merit_stage(p, k, xk, uk, yr, ye, bb, NUk, ETAk), c.gs);
@@ -1582,9 +1588,9 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     while (__ballot(!fin) != 0ull) {
         double xt[4], ut[2], xnx[4], def[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xt[q] = xk[q] + alpha * dxk[q];
-        ut[0] = uk[0] + alpha * duk[0];
-        ut[1] = uk[1] + alpha * duk[1];
+        for (int q = 0; q < 4; ++q) xt[q] = qfma(alpha, dxk[q], xk[q]);
+        ut[0] = qfma(alpha, duk[0], uk[0]);
+        ut[1] = qfma(alpha, duk[1], uk[1]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) xnx[q] = wave_from_next(xt[q]);   // x_{k+1} + alpha dx_{k+1}
         if (stg) {
@@ -1598,7 +1604,7 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
         }
         const double phi = group_sum(merit_stage(p, k, xt, ut, yr, ye, def, NUk, ETAk), c.gs);
         if (!fin) {
-            if (phi <= phi0 + p.ls_eps * alpha * dphi) {
+            if (phi <= qfma(p.ls_eps * alpha, dphi, phi0)) {
                 fin = true;
             } else {
                 const double an = alpha * p.ls_alpha_red;
@@ -1609,20 +1615,20 @@ __global__ void __launch_bounds__(64) merit_ls_kernel(SolveArgs A) {
     }
     if (skip) return;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) X[4 * k + q] = xk[q] + alpha * dxk[q];
+    for (int q = 0; q < 4; ++q) X[4 * k + q] = qfma(alpha, dxk[q], xk[q]);
     if (stg) {
-        U[2 * k] = uk[0] + alpha * duk[0];
-        U[2 * k + 1] = uk[1] + alpha * duk[1];
+        U[2 * k] = qfma(alpha, duk[0], uk[0]);
+        U[2 * k + 1] = qfma(alpha, duk[1], uk[1]);
         double* nw = A.wnlp + si;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const double pk = nw[(W_PI + q) * tot];
-            nw[(W_PI + q) * tot] = pk + alpha * (w[(Q_PI + q) * tot] - pk);
+            nw[(W_PI + q) * tot] = qfma(alpha, w[(Q_PI + q) * tot] - pk, pk);
         }
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
             const double lk = nw[(W_LAM + q) * tot];
-            nw[(W_LAM + q) * tot] = lk + alpha * (w[(Q_LAM + q) * tot] - lk);
+            nw[(W_LAM + q) * tot] = qfma(alpha, w[(Q_LAM + q) * tot] - lk, lk);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) nw[(W_NU + q) * tot] = NUk[q];
@@ -1645,17 +1651,18 @@ __global__ void epilogue_kernel(SolveArgs A) {
     double cost = 0.0;
     for (int k = 0; k < N; ++k) {
         double s = 0.0;
-        for (int q = 0; q < 4; ++q) { const double r = X[4 * k + q] - yref[6 * k + q]; s += p.W[q] * r * r; bad |= !isfinite(X[4 * k + q]); }
-        for (int q = 0; q < 2; ++q) { const double r = U[2 * k + q] - yref[6 * k + 4 + q]; s += p.W[4 + q] * r * r; bad |= !isfinite(U[2 * k + q]); }
-        cost += 0.5 * p.tau * s;
+        for (int q = 0; q < 4; ++q) { const double r = X[4 * k + q] - yref[6 * k + q]; s = qfma(p.W[q] * r, r, s); bad |= !isfinite(X[4 * k + q]); }
+        for (int q = 0; q < 2; ++q) { const double r = U[2 * k + q] - yref[6 * k + 4 + q]; s = qfma(p.W[4 + q] * r, r, s); bad |= !isfinite(U[2 * k + q]); }
+        cost = qfma(0.5 * p.tau, s, cost);
     }
     double s = 0.0;
-    for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s += p.We[q] * r * r; bad |= !isfinite(X[4 * N + q]); }
-    cost += 0.5 * s;
+    for (int q = 0; q < 4; ++q) { const double r = X[4 * N + q] - ye[q]; s = qfma(p.We[q] * r, r, s); bad |= !isfinite(X[4 * N + q]); }
+    cost = qfma(0.5, s, cost);
     A.cost[i] = cost;
-    // wdone: 1 converged, 2 failed QP, 3 infeasible stage-0 bound (sqp_iter written then)
+    // wdone: 1 converged, 2 non-finite QP solution, 3 infeasible stage-0 bound, 4 diverged QP
+    // (sqp_iter written then)
     const int fr = A.wdone ? A.wdone[i] : 0;
-    if (fr == 3) A.status[i] = QSP_STATUS_QP_FAIL;
+    if (fr == 3 || fr == 4) A.status[i] = QSP_STATUS_QP_FAIL;
     else if (p.nlp_mode == 1) A.status[i] = (bad || fr == 2) ? 1 : (fr == 1 ? 0 : 2);
     else A.status[i] = (bad || fr == 2) ? 1 : 0;
     if (fr == 0) A.sqp_iter[i] = p.sqp_iters;
@@ -1697,7 +1704,7 @@ __device__ __forceinline__ double contact_phi(const ShapeDev& sh, double s, doub
     SplineEval e;
     spline_eval(sh, mat_mod(s, sh.b), e);
     const double ex = e.C[0] - px, ey = e.C[1] - py;
-    return ex * ex + ey * ey;
+    return qfma(ey, ey, ex * ex);
 }
 
 // The contact point after a lateral disturbance: argmin_s |C(s) - p|^2 from s0 (fminunc in the
@@ -1708,8 +1715,8 @@ __device__ double reproject_contact(const ShapeDev& sh, double px, double py, do
         SplineEval e;
         spline_eval(sh, mat_mod(s, sh.b), e);
         const double ex = e.C[0] - px, ey = e.C[1] - py;
-        const double g = 2.0 * (ex * e.D[0] + ey * e.D[1]);
-        const double h = 2.0 * (e.D[0] * e.D[0] + e.D[1] * e.D[1] + ex * e.Dd[0] + ey * e.Dd[1]);
+        const double g = 2.0 * qfma(ey, e.D[1], ex * e.D[0]);
+        const double h = 2.0 * qfma(ey, e.Dd[1], qfma(ex, e.Dd[0], qfma(e.D[1], e.D[1], e.D[0] * e.D[0])));
         if (fabs(g) < 1e-14) break;
         double step = h > 0.0 ? -g / h : (g > 0.0 ? -0.05 : 0.05) * sh.b;
         const double smax = 0.25 * sh.b;
@@ -1748,7 +1755,7 @@ __global__ void closed_loop_pre_kernel(ClosedLoopArgs a, int t) {
         SplineEval e;
         spline_eval(sh, mat_mod(x[3], sh.b), e);
         const double sn = reproject_contact(sh, -0.5 * sh.xwidth, e.C[1] - amp, 0.0);
-        x[3] = mat_mod(sn, sh.b) - sh.b * (sn < 0.0 ? 1.0 : 0.0);
+        x[3] = qfma(-sh.b, sn < 0.0 ? 1.0 : 0.0, mat_mod(sn, sh.b));
     }
     if (a.noise)
         for (int c = 0; c < 4; ++c) x[c] += a.noise[((size_t)t * a.B + i) * 4 + c];
@@ -1761,7 +1768,7 @@ __global__ void closed_loop_pre_kernel(ClosedLoopArgs a, int t) {
         const double* u = a.ubc + ((size_t)i * a.D + (a.D - k)) * 2;
         DynOut d;
         dynamics<false>(sh, x[2], x[3], u[0], u[1], d);
-        for (int c = 0; c < 4; ++c) x[c] += a.Ts * d.f[c];
+        for (int c = 0; c < 4; ++c) x[c] = qfma(a.Ts, d.f[c], x[c]);
     }
     for (int c = 0; c < 4; ++c) a.xs[(size_t)i * 4 + c] = x[c];
     if (a.Xsim)
@@ -1793,7 +1800,7 @@ __global__ void plant_kernel(ClosedLoopArgs a, int t) {
     DynOut d;
     dynamics<false>(sh, xi[2], xi[3], ua[0], ua[1], d);
     for (int c = 0; c < 4; ++c) {
-        const double v = xi[c] + a.Ts * d.f[c];
+        const double v = qfma(a.Ts, d.f[c], xi[c]);
         a.x[(size_t)i * 4 + c] = v;
         if (t + 1 == a.n_steps) a.Xtraj[((size_t)i * (a.n_steps + 1) + t + 1) * 4 + c] = v;
     }
@@ -1812,7 +1819,7 @@ __global__ void delay_sim_kernel(ClosedLoopArgs a) {
         const double* u = a.ubc + ((size_t)i * a.D + (a.D - k)) * 2;
         DynOut d;
         dynamics<false>(sh, x[2], x[3], u[0], u[1], d);
-        for (int c = 0; c < 4; ++c) x[c] += a.Ts * d.f[c];
+        for (int c = 0; c < 4; ++c) x[c] = qfma(a.Ts, d.f[c], x[c]);
     }
     for (int c = 0; c < 4; ++c) a.xs[(size_t)i * 4 + c] = x[c];
 }
@@ -1854,7 +1861,7 @@ hipError_t launch_reproject(const ShapeDev* shapes, int n_shapes, const int32_t*
 // quintic over tf / 2 and then holds its final value (:58-66).
 __device__ __forceinline__ double quintic(double t, double tf) {
     const double tau = t / tf;
-    return ((6.0 * tau - 15.0) * tau + 10.0) * tau * tau * tau;
+    return qfma(qfma(6.0, tau, -15.0), tau, 10.0) * tau * tau * tau;
 }
 
 __global__ void straight_lines_kernel(int B, int T, const double* x0, const double* xf, double t0, double tf,
@@ -1862,20 +1869,20 @@ __global__ void straight_lines_kernel(int B, int T, const double* x0, const doub
     const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (size_t)B * T) return;
     const int i = (int)(g / T), k = (int)(g - (size_t)i * T);
-    const double t = t0 + k * Ts;
+    const double t = qfma((double)k, Ts, t0);
     const double* a = x0 + (size_t)i * 3;
     const double* b = xf + (size_t)i * 3;
     const double s = quintic(t, tf);
     double* out = traj + g * 6;
-    out[0] = a[0] + s * (b[0] - a[0]);
-    out[1] = a[1] + s * (b[1] - a[1]);
+    out[0] = qfma(s, b[0] - a[0], a[0]);
+    out[1] = qfma(s, b[1] - a[1], a[1]);
     if (auto_angle) {
         const double tfa = 0.5 * tf;
         const int ka = (int)floor((tfa - t0) / Ts + 1e-9);      // last sample of t0:Ts:tf/2
-        const double ta = t0 + (k < ka ? k : ka) * Ts;
-        out[2] = a[2] + quintic(ta, tf) * (b[2] - a[2]);
+        const double ta = qfma((double)(k < ka ? k : ka), Ts, t0);
+        out[2] = qfma(quintic(ta, tf), b[2] - a[2], a[2]);
     } else {
-        out[2] = a[2] + s * (b[2] - a[2]);
+        out[2] = qfma(s, b[2] - a[2], a[2]);
     }
     out[3] = 0.0;
     out[4] = 0.0;
@@ -1899,7 +1906,7 @@ __global__ void spline_kernel(const ShapeDev* shapes, const int32_t* sid, int n,
     SplineEval e;
     spline_eval(sh, s[i], e);
     for (int c = 0; c < 2; ++c) { C[2 * i + c] = e.C[c]; D[2 * i + c] = e.D[c]; Dd[2 * i + c] = e.Dd[c]; }
-    kappa[i] = (e.D[0] * e.Dd[1] - e.D[1] * e.Dd[0]) / (e.D[0] * e.D[0] + e.D[1] * e.D[1]);
+    kappa[i] = angle_rate_of(e);
 }
 
 __global__ void dynamics_kernel(const ShapeDev* shapes, const int32_t* sid, int n, const double* x, const double* u,

@@ -13,7 +13,8 @@ import numpy as np
 def closed_loop_matlab(plant, controller, x0, time_sim, print_=False, sim_noise=False, debug_cost=False,
                        disturbance_=False, amplitude_dist=0.0, t_dist=0, seed=0):
     """Returns (x_s, x_sim, y_s, theta_s, S_p_x, S_p_y, u_n, u_t, time_sim_vec, mode_vect, found_sol),
-    each with a leading batch dimension B (helper.m:195-197); amplitude_dist may be per lane."""
+    each with a leading batch dimension B (helper.m:195-197; x_sim is (B, 2T+1, 4): the reference's
+    4 x (2T+1) with its T+1 leading zero columns); amplitude_dist may be per lane."""
     Ts = controller.sample_time
     time_sim_vec = np.arange(0.0, time_sim + 1e-9, Ts)                      # :198
     T = len(time_sim_vec)
@@ -30,5 +31,7 @@ def closed_loop_matlab(plant, controller, x0, time_sim, print_=False, sim_noise=
     found_sol = r["status"] == 0                                            # :253-260
     S_p = plant.SP.FC(X[:, :, 3].ravel()).reshape(B, T, 2)                 # :316-318
     mode_vect = np.zeros((B, T), dtype="<U1")
-    return (X[:, :, 0], r["Xsim"], X[:, :, 1], X[:, :, 2], S_p[..., 0], S_p[..., 1], U[:, :, 0], U[:, :, 1],
+    # x_sim = [zeros(nx, T+1) xk_sim ...] (helper.m:203, :247): T + 1 zero columns, then one per step
+    x_sim = np.concatenate([np.zeros((B, T + 1, 4)), r["Xsim"]], 1)
+    return (X[:, :, 0], x_sim, X[:, :, 1], X[:, :, 2], S_p[..., 0], S_p[..., 1], U[:, :, 0], U[:, :, 1],
             time_sim_vec, mode_vect, found_sol)

@@ -24,6 +24,7 @@ class OcpSolver:
     def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
                  cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10,
                  qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=True, qp_stall_iters=3, qp_stall_alpha=1e-3,
+                 qp_mu_max=1e100,
                  nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
                  timings=False):
         L = _lib.lib()
@@ -37,6 +38,7 @@ class OcpSolver:
         o.qp_tol_stat, o.qp_tol_eq = float(qp_tol_stat), float(qp_tol_eq)
         o.stage0_s_bound = 1 if stage0_s_bound else 0
         o.qp_stall_iters, o.qp_stall_alpha = int(qp_stall_iters), float(qp_stall_alpha)
+        o.qp_mu_max = float(qp_mu_max)
         if nlp_solver_type not in self.NLP_MODES:
             raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
         o.nlp_mode = self.NLP_MODES[nlp_solver_type]
@@ -194,10 +196,11 @@ class OcpSolver:
             fn = {"x": self._L.qsp_get_x, "u": self._L.qsp_get_u, "pi": self._L.qsp_get_pi}[field]
             check(fn(self._h, ptr(out)), f"get('{field}')")
             return out if stage is None else out[:, stage]
-        if field in ("status", "sqp_iter", "qp_iter", "qp_capped"):
+        if field in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
             out = np.zeros(B, np.int32)
             fn = {"status": self._L.qsp_get_status, "sqp_iter": self._L.qsp_get_sqp_iter,
-                  "qp_iter": self._L.qsp_get_qp_iter, "qp_capped": self._L.qsp_get_qp_capped}[field]
+                  "qp_iter": self._L.qsp_get_qp_iter, "qp_capped": self._L.qsp_get_qp_capped,
+                  "qp_stalled": self._L.qsp_get_qp_stalled}[field]
             check(fn(self._h, ptr(out)), f"get('{field}')")
             return out
         if field == "time_tot":
