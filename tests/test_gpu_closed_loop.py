@@ -192,10 +192,12 @@ def test_closed_loop_disturbance_matches_oracle(oracle):
                                        dist_amp=amp, xwidth=xw)
     ref, st = _stable_lanes(oracle, run, x0)
     assert st.mean() > 0.5, st.mean()
-    # the disturbed state itself (step td, before the solve) on every lane: x, y, theta exactly as
-    # the oracle; the re-projected s to 1e-6 (a target near a circular arc's centre makes the
-    # minimiser flat: the two spline formulations then stop a little apart)
-    np.testing.assert_allclose(r["X"][:, td - 1, :3], ref["X"][:, td - 1, :3], rtol=0, atol=1e-10)
+    # the disturbed state itself (step td, before the solve): x, y, theta as the literal oracle to
+    # 1e-8 on the stable lanes (the first td - 1 closed-loop steps carry the two formulations'
+    # rounding differences; bit-for-bit equality with the kernel-order twin is
+    # tests/test_gpu_twin.py::test_closed_loop_bit_identical); the re-projected s to 1e-6 (a target
+    # near a circular arc's centre makes the minimiser flat: the formulations stop a little apart)
+    np.testing.assert_allclose(r["X"][st, td - 1, :3], ref["X"][st, td - 1, :3], rtol=0, atol=1e-8)
     np.testing.assert_allclose(r["X"][:, td - 1, 3], ref["X"][:, td - 1, 3], rtol=0, atol=1e-6)
     assert np.abs(r["U"] - ref["U"]).max(axis=(1, 2))[st].max() < 1e-6
     assert np.abs(r["X"] - ref["X"]).max(axis=(1, 2))[st].max() < 1e-8

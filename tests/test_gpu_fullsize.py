@@ -32,7 +32,7 @@ def test_config3_shuffle_invariance_and_bounds():
     s.set_shape_ids(sid)
     u1 = s.controller_solve(x0, 1)
     st = s.get("status")
-    capped = s.get("qp_capped")
+    capped = s.get("qp_capped") + s.get("qp_stalled")   # QPs that returned their last iterate
     s.controller_reset()
     u2 = s.controller_solve(x0, 1)
     perm = np.random.default_rng(1).permutation(B)
@@ -45,7 +45,7 @@ def test_config3_shuffle_invariance_and_bounds():
     np.testing.assert_array_equal(u3, u1[perm])
     # u0 satisfies its bounds on every lane whose QPs all met the stop test (HPIPM-style: mu,
     # bound, stationarity and equality residuals); only a full step from a QP stopped by the
-    # iteration cap (qp_iters 50, its last iterate used as HPIPM's at iter_max) may leave one
+    # iteration cap or the stall exit (its last iterate used, as HPIPM's at iter_max) may leave one
     viol = np.maximum.reduce([-u1[:, 0], u1[:, 0] - 0.03, np.abs(u1[:, 1]) - 0.05])
     assert np.all(capped[viol > 1e-9] > 0), np.sort(viol[capped == 0])[-5:]
     assert np.mean(viol > 1e-9) < 2e-4, (np.sum(viol > 1e-9), np.sort(viol)[-5:])
