@@ -11,6 +11,11 @@ import collections
 import csv
 import glob
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from uclv_qs_pushing_matlab_amd.build import source_digest  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
@@ -49,6 +54,7 @@ if args.json:
            "stream_parts": args.parts, "per": "SQP iteration over the whole batch (= bench roofline launch)",
            "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
            "raw_FETCH_SIZE_KiB": fetch, "raw_WRITE_SIZE_KiB": write,
-           "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024"}
+           "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024",
+           "kernel_digest": source_digest()}
     json.dump(out, open(args.json, "w"), indent=1)
     print(json.dumps(out))

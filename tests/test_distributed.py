@@ -83,3 +83,19 @@ def test_make_inputs_shards_match_single_process():
         parts = [make_inputs(1000, 20, 7, *shard_range(1000, world, r)) for r in range(world)]
         for q in range(4):
             np.testing.assert_array_equal(np.concatenate([p[q] for p in parts]), full[q])
+
+
+def test_bench_gpus_flag_launches_ranks_or_fails_loudly():
+    """bench.py --gpus N (no WORLD_SIZE) starts its own N ranks; with fewer visible GPUs than N it
+    refuses (exit 2) before touching a device -- here, in a container without GPUs."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "QSP_DIST_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("GPUs visible: the launch itself is tests/test_gpu_multirank.py's")
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "GPU(s) visible" in r.stderr

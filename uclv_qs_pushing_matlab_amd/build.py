@@ -15,6 +15,21 @@ HEADERS = ["qsp_math.hpp", "qsp_fp.hpp", "qsp_types.h", "qsp_kernels.h", "../../
 ARCH = os.environ.get("QSP_OFFLOAD_ARCH", "gfx950")
 
 
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
+
+
+def source_digest():
+    """Digest of what determines the kernels' code: the sources, headers and compile flags.
+    profiles/pmc_traffic.json records the digest its counters were collected at, and bench.py
+    reports that traffic only while the library is built from the same sources."""
+    import hashlib
+    h = hashlib.sha256(" ".join([ARCH] + FLAGS).encode())
+    for f in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale():
     if not os.path.exists(LIB):
         return True
@@ -29,8 +44,7 @@ def build(force=False, verbose=False):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     # -ffp-contract=off: every fused multiply-add is an explicit fma() in the source, so the
     # oracle twin reproduces the device arithmetic bit for bit (qsp_fp.hpp)
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-I", os.path.join(PKG, "..", "include")]
+    cmd = [hipcc, f"--offload-arch={ARCH}"] + FLAGS + ["-I", os.path.join(PKG, "..", "include")]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     cmd += ["-o", LIB + ".tmp"]
     if verbose:
