@@ -196,9 +196,10 @@ def test_closed_loop_disturbance_matches_oracle(oracle):
     # 1e-8 on the stable lanes (the first td - 1 closed-loop steps carry the two formulations'
     # rounding differences; bit-for-bit equality with the kernel-order twin is
     # tests/test_gpu_twin.py::test_closed_loop_bit_identical); the re-projected s to 1e-6 (a target
-    # near a circular arc's centre makes the minimiser flat: the formulations stop a little apart)
+    # near a circular arc's centre makes the minimiser flat: the formulations' Newton iterations stop
+    # a little apart -- measured up to 2.7e-6 since the explicit-FMA formulation, 1e-6 before)
     np.testing.assert_allclose(r["X"][st, td - 1, :3], ref["X"][st, td - 1, :3], rtol=0, atol=1e-8)
-    np.testing.assert_allclose(r["X"][:, td - 1, 3], ref["X"][:, td - 1, 3], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(r["X"][:, td - 1, 3], ref["X"][:, td - 1, 3], rtol=0, atol=1e-5)
     assert np.abs(r["U"] - ref["U"]).max(axis=(1, 2))[st].max() < 1e-6
     assert np.abs(r["X"] - ref["X"]).max(axis=(1, 2))[st].max() < 1e-8
     # the re-projected s is wrapped into [-b, b) (helper.m:233)
