@@ -753,7 +753,10 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
     // (x / 0 = inf: a residual that starts at zero never binds)
     double rs_stop = p.res_stop / group_max(r0, c.gs);
     const double rs_g = p.qp_tol_stat / group_max(rg0, c.gs), rs_b = p.qp_tol_eq / group_max(rb0, c.gs);
-    rs_stop = rs_g < rs_stop ? rs_g : rs_stop;   // (as the oracle: a NaN start residual keeps NaN)
+    // a NaN start residual compares false here and leaves rs_stop as it was (the fmax accumulation
+    // above drops NaN anyway); a NaN QP is caught by the divergence exit (NaN mu) or the non-finite
+    // solution check after the loop, not by this threshold
+    rs_stop = rs_g < rs_stop ? rs_g : rs_stop;
     rs_stop = rs_b < rs_stop ? rs_b : rs_stop;
     double rscale = 1.0;
     int nit = 0, stall = 0;
