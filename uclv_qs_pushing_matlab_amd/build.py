@@ -19,14 +19,19 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 
 
 def source_digest():
-    """Digest of what determines the kernels' code: the sources, headers and compile flags.
-    profiles/pmc_traffic.json records the digest its counters were collected at, and bench.py
-    reports that traffic only while the library is built from the same sources."""
+    """Digest of what determines the kernels' code: the sources and headers with their comments
+    and whitespace stripped, and the compile flags.  profiles/pmc_traffic.json records the digest
+    its counters were collected at, and bench.py reports that traffic only while the library is
+    built from the same code."""
     import hashlib
+    import re
     h = hashlib.sha256(" ".join([ARCH] + FLAGS).encode())
     for f in SOURCES + HEADERS:
-        with open(os.path.join(CSRC, f), "rb") as fh:
-            h.update(fh.read())
+        with open(os.path.join(CSRC, f)) as fh:
+            src = fh.read()
+        src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)      # block comments
+        src = re.sub(r"//[^\n]*", " ", src)                     # line comments
+        h.update(" ".join(src.split()).encode())
     return h.hexdigest()[:16]
 
 
