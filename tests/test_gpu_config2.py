@@ -51,7 +51,15 @@ def test_config2_exact_law_parity(oracle):
     capped = s.get("qp_capped")
     s.close()
     assert np.all(status == 0)
-    assert capped.sum() < 0.01 * B * K          # QPs stopped by the cap (qp_iters 20) or stalled are rare
+    assert capped.sum() < 0.01 * B * K          # QPs stopped by the cap (qp_iters 20) are rare
+    # the device-resident path (qsp_solve_device, the bench's) against the kernel-order twin: every
+    # lane bit for bit
+    from oracle.oracle import Oracle
+    tw = Oracle(NAMES, twin=True)
+    rt = tw.controller_solve(make_opts(N=N, sqp_iters=K), x0, traj, 1, tw.new_warm(B, N), shape_id=sid)
+    np.testing.assert_array_equal(u0, rt["u0"])
+    np.testing.assert_array_equal(status, rt["status"])
+    np.testing.assert_array_equal(capped, rt["qp_capped"])
 
     def run(xx, **kw):
         return oracle.controller_solve(make_opts(N=N, sqp_iters=K, **kw), xx, traj, 1, oracle.new_warm(len(xx), N),

@@ -4,7 +4,8 @@ shards of 32 768 lanes that bench.py gives the ranks of an 8-GPU node (sharding.
 
 * every shard's u0 and status equal the same lanes of the whole-batch solve bit for bit (lanes are
   independent; the 8-GPU run differs from this only in where the shards execute);
-* lanes from every shard agree with the oracle on the lanes the oracle itself reproduces (the
+* every one of the 262 144 lanes equals the oracle's kernel-order twin bit for bit (u0, status);
+* lanes from every shard agree with the literal oracle on the lanes it itself reproduces (the
   probe criterion of tests/test_gpu_config2.py)."""
 import numpy as np
 import pytest
@@ -46,6 +47,11 @@ def test_config3_eight_shards_k50(oracle):
         np.testing.assert_array_equal(st, st_all[lo:hi])
         picks.append(np.r_[lo:lo + 48, hi - 16:hi])              # both ends of every shard
     idx = np.concatenate(picks)
+    from oracle.oracle import Oracle
+    tw = Oracle(NAMES, twin=True)
+    rt = tw.controller_solve(make_opts(N=N, sqp_iters=K), x0, traj, 1, tw.new_warm(total, N), shape_id=sid)
+    np.testing.assert_array_equal(u_all, rt["u0"])
+    np.testing.assert_array_equal(st_all, rt["status"])
 
     def run(xx, **kw):
         return oracle.controller_solve(make_opts(N=N, sqp_iters=K, **kw), xx, traj, 1, oracle.new_warm(len(xx), N),
