@@ -577,18 +577,6 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             st.kk[0][1] = qfma(Rn[2], rt[1], qfma(Rn[1], rt[0], st.kk[0][1]));
         }
     } else
-#ifdef QSP_EXPERIMENT_WALK_REPS
-    // Developer experiment only (scripts/mkvariant.sh): the factor walk run
-    // QSP_EXPERIMENT_WALK_REPS times (each pass recomputes the same factors from the terminal value
-    // function), so the time difference to the production kernel is the walk's own cost at unchanged
-    // numerics and IPM counts.
-    for (int rep = 0; rep < (FACTOR ? QSP_EXPERIMENT_WALK_REPS : 1); ++rep) {
-    if (rep > 0) {
-#pragma unroll
-        for (int ls = 0; ls < S; ++ls)
-            if (ls == lsN) ric_terminal(p, st.g[ls], P, pv);
-    }
-#endif
     for (int j = c.L - 1; j >= 0; --j) {
         // Lanes above j already hold their final factors and sit the step out (exec
         // mask); lanes below j compute a throw-away step that their own turn overwrites.
@@ -631,9 +619,6 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             }
         }
     }
-#ifdef QSP_EXPERIMENT_WALK_REPS
-    }
-#endif
     if constexpr (S == 1) {
         // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
         // one 4x4 affine map (16 FMA) instead of du = kk + K dx followed by the dynamics;
