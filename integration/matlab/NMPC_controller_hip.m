@@ -20,7 +20,7 @@ classdef NMPC_controller_hip < handle
             self.Hp = Hp; self.T = Hp*sample_time; self.B = B;
             self.ocp_opts = struct('nlp_solver_type', 'SQP', 'nlp_solver_max_iter', 30, ...
                 'nlp_solver_tol_stat', 1e-6, 'nlp_solver_tol_eq', 1e-6, 'nlp_solver_tol_ineq', 1e-6, ...
-                'nlp_solver_tol_comp', 1e-6);                                  % NMPC_controller.m:271-276
+                'nlp_solver_tol_comp', 1e-6, 'qp_solver_cond_N', 5);           % NMPC_controller.m:271-276
         end
         function create_ocp_solver(self, shapes, shape_id)                  % :302-305
             % shapes: n x 7 cell {ply_path, flip, mu_sg, mu_sp, m, tau_max, xwidth}; shape_id: 1 x B (0-based)

@@ -12,7 +12,7 @@
  *        nlp_solver_max_iter (30 for SQP, 1 for SQP_RTI), nlp_solver_tol_stat/eq/ineq/comp (1e-6),
  *        qp_solver_iter_max (20), globalization_alpha_min (0.05), globalization_alpha_reduction
  *        (0.7), eps_sufficient_descent (1e-4), stage0_s_bound (1), stages_per_lane (0 = auto),
- *        device (0)                                      -- NMPC_controller.m:270-300
+ *        device (0), qp_solver_cond_N (1..N; validated only, see below)  -- NMPC_controller.m:270-300
  *   d = qsp_nmpc_mex('dims', h)                          % [N B]
  *   qsp_nmpc_mex('shape_ply', h, {ply, flip, mu_sg, mu_sp, m, tau_max, xwidth; ...}, shape_id)
  *   qsp_nmpc_mex('set', h, field, value [, stage])
@@ -118,6 +118,12 @@ static void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[
     o.stage0_s_bound = (int32_t)opt_num(op, "stage0_s_bound", o.stage0_s_bound);
     o.stages_per_lane = (int32_t)opt_num(op, "stages_per_lane", 0);
     o.device = (int32_t)opt_num(op, "device", 0);
+    /* qp_solver_cond_N (NMPC_controller.m:276, 5 there) picks HPIPM's partial condensing: a different
+     * factorisation of the same QP, so the solution does not depend on it.  The library always
+     * factorises stage-wise, which measured 1.16-3.1x faster than condensed blocks at N = 20 and 50
+     * (profiles/r03/cond_block.txt); the field is accepted for drop-in option structs and checked. */
+    const double cn = opt_num(op, "qp_solver_cond_N", o.N);
+    if (cn != floor(cn) || cn < 1 || cn > o.N) mexErrMsgIdAndTxt("qsp:args", "qp_solver_cond_N: an integer in 1..N");
     qsp_solver* h = NULL;
     check(qsp_create(&o, &h), "qsp_create");
     if (qsp_set_timing(h, 1) != QSP_OK) {   /* acados reports time_lin / time_qp_sol for every solve */

@@ -35,3 +35,12 @@ def test_waypoints_config1_is_linear():
     assert len(t) == 201
     np.testing.assert_allclose(traj[0], 0.01 * t, atol=1e-15)
     np.testing.assert_allclose(traj[1:], 0.0, atol=1e-15)
+
+
+def test_qp_solver_cond_N_checked_before_any_device_call():
+    # NMPC_controller.m:276 sets 5; out-of-range values fail as acados rejects them (no GPU needed:
+    # the check precedes library loading)
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    for bad in (0, 21, 2.5, -1):
+        with pytest.raises(ValueError):
+            OcpSolver(N=20, qp_solver_cond_N=bad)

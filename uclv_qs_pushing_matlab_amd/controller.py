@@ -20,7 +20,7 @@ from .solver import OcpSolver
 
 class NMPCController:
     def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=20,
-                 device=0, stages_per_lane=0):
+                 device=0, stages_per_lane=0, qp_solver_cond_N=5):
         # create_ocp_opts (:270-300): 'SQP' with merit backtracking, max_iter 30, tol 1e-6;
         # nlp_solver_type='SQP_RTI' gives the fixed-K full-step iteration of the BASELINE metric
         self.name = name
@@ -44,8 +44,9 @@ class NMPCController:
         self.initial_condition = np.zeros((self.batch, 4))
         self.y_ref = None
         self.cost_function_vect = []
+        # qp_solver_cond_N = 5 as :276 (checked, same QP solution; OcpSolver's note)
         self._opts = dict(nlp_solver_type=nlp_solver_type, sqp_iters=sqp_iters, qp_iters=qp_iters, device=device,
-                          stages_per_lane=stages_per_lane)
+                          stages_per_lane=stages_per_lane, qp_solver_cond_N=min(qp_solver_cond_N, self.Hp))
         self.ocp_solver = None
         self._shape_id = np.zeros(self.batch, np.int32)
 

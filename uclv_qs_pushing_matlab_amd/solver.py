@@ -26,7 +26,15 @@ class OcpSolver:
                  qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=True, qp_stall_iters=3, qp_stall_alpha=1e-3,
                  qp_mu_max=1e100,
                  nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
-                 timings=False):
+                 qp_solver_cond_N=None, timings=False):
+        # qp_solver_cond_N (NMPC_controller.m:276) selects HPIPM's partial condensing, a different
+        # factorisation of the same QP.  The kernel factorises stage-wise at every value: condensed
+        # blocks measured 1.16-3.1x slower (profiles/r03/cond_block.txt).  The
+        # value is checked (1..N) and kept as .qp_solver_cond_N.
+        if qp_solver_cond_N is not None and (int(qp_solver_cond_N) != qp_solver_cond_N
+                                             or not 1 <= qp_solver_cond_N <= N):
+            raise ValueError("qp_solver_cond_N must be an integer in 1..N")
+        self.qp_solver_cond_N = int(N if qp_solver_cond_N is None else qp_solver_cond_N)
         L = _lib.lib()
         o = _lib.Options()
         L.qsp_default_options(C.byref(o))
