@@ -252,3 +252,20 @@ def test_delay_buffer_mirror(oracle):
         f, _ = oracle.dynamics(ref, u)
         ref = ref + 0.05 * f
     np.testing.assert_allclose(xs, ref, rtol=0, atol=1e-12)
+
+
+def test_closed_loop_bench_line():
+    """bench.py --closed-loop (SURVEY §8(f) row 1 measured): one JSON line, every sampled closed loop
+    bit-identical to the twin's (X, U, status over all 201 steps of main.m's scenario)."""
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--closed-loop", "--global-batch", "192",
+                          "--steps", "1", "--cpu-seconds", "1"], capture_output=True, text=True, timeout=200, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["unit"] == "lane-steps/s" and d["value"] > 0
+    p = d["parity"]
+    assert p["lanes"] >= 16 and p["bit_identical_trajectory_lanes"] == p["lanes"], p
