@@ -196,25 +196,24 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None):
     return out
 
 
-def closed_loop_bench(args):
+def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
     """SURVEY §8(f) row 1, measured: helper.closed_loop_matlab as main.m runs it (helper.m:195-322;
     main.m:40-41, 105, 150-205): Hp = 10, the reference's SQP options (sqp + merit backtracking,
     max_iter 30, tol 1e-6), time_sim 10 s (201 steps of Ts = 0.05), the 2-waypoint straight line,
     no noise, no delays, the disturbance step t_dist = 15 / Ts (past the end of the run, as in main.m)
     -- batched over B lanes (x0 from the config-2 law, 4 shapes mixed per lane), the whole loop on
-    the device in one host call (qsp_closed_loop_ex).  One JSON line: lane-steps/s, the twin's closed
-    loop on the host threads as the CPU baseline, and every sampled lane's trajectory (X, U, status)
+    the device in one host call (qsp_closed_loop_ex).  Returns lane-steps/s, the twin's closed loop
+    on the host threads as the CPU baseline, and every sampled lane's trajectory (X, U, status)
     against the twin bit for bit."""
     import torch
     from uclv_qs_pushing_matlab_amd.objects import make_shape
     from uclv_qs_pushing_matlab_amd.solver import OcpSolver
     N, K, Ts, T = 10, 30, 0.05, 201
-    B = args.global_batch or CONFIG2_BATCH
-    x0 = config2_x0(B, args.seed)
+    x0 = config2_x0(B, seed)
     sid = (np.arange(B) % len(SHAPES)).astype(np.int32)
     traj = straight_traj()
     t_dist = int(round(15 / Ts))
-    s = OcpSolver(N=N, batch=B, sqp_iters=K, nlp_solver_type="SQP", device=0)
+    s = OcpSolver(N=N, batch=B, sqp_iters=K, nlp_solver_type="SQP", device=device)
     s.set_shapes([make_shape(n) for n in SHAPES], shape_id=sid)
     s.set_reference_trajectory(traj)
     S_layout, L_layout = s.layout()
@@ -222,51 +221,59 @@ def closed_loop_bench(args):
     s.synchronize()
     torch.cuda.synchronize()
     times = []
-    for _ in range(max(1, args.steps)):
+    for _ in range(max(1, runs)):
         t0 = time.perf_counter()
         r = s.closed_loop(x0, T, disturbance=True, t_dist=t_dist)
         times.append(time.perf_counter() - t0)
     s.close()
     el = float(np.median(times))
-    result = {"metric": "closed-loop controller steps/s (helper.closed_loop_matlab, main.m scenario)",
-              "value": B * T / el, "unit": "lane-steps/s", "n_gpus": 1, "steps": len(times), "warmup": 1,
-              "ms_per_step": el * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-              "dtype": "f64", "data": "synthetic",
-              "config": {"workload": f"{B} closed loops of {T} steps (main.m: Hp=10, sqp + merit backtracking, "
-                                     "max_iter 30, tol 1e-6, straight-line reference, no noise, no delay, "
-                                     "t_dist past the end), 4 shapes mixed per lane, x0 from the config-2 law, "
-                                     "whole loop on the device (qsp_closed_loop_ex, one host call; "
-                                     "trajectories copied back inside the timed region)",
-                         "batch": B, "N": N, "sqp_max_iter": K, "closed_loop_steps": T,
-                         "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout}},
-              "status_lane_steps": {str(int(k)): int(v) for k, v in zip(*np.unique(r["status"], return_counts=True))},
-              "status_note": "acados codes per controller step: 0 converged, 2 max_iter reached, 4 QP failure "
-                             "(stage-0 s outside its bounds, or a diverged QP); helper.m applies u0 regardless"}
-    if not args.no_cpu:
+    out = {"workload": f"{B} closed loops of {T} steps (main.m: Hp=10, sqp + merit backtracking, max_iter 30, "
+                       "tol 1e-6, straight-line reference, no noise, no delay, t_dist past the end), 4 shapes mixed "
+                       "per lane, x0 from the config-2 law, whole loop on the device (qsp_closed_loop_ex, one host "
+                       "call; trajectories copied back inside the timed region)",
+           "gpu_lane_steps_per_s": B * T / el, "ms_per_run": el * 1e3, "runs": len(times),
+           "batch": B, "N": N, "sqp_max_iter": K, "closed_loop_steps": T,
+           "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout},
+           "status_lane_steps": {str(int(k)): int(v) for k, v in zip(*np.unique(r["status"], return_counts=True))},
+           "status_note": "acados codes per controller step: 0 converged, 2 max_iter reached, 4 QP failure "
+                          "(stage-0 s outside its bounds, or a diverged QP); helper.m applies u0 regardless"}
+    if not no_cpu:
         from oracle.oracle import Oracle, make_opts
         hc = host_cpu()
         threads = hc["threads"]
         tw = Oracle(SHAPES, twin=True)
         op = make_opts(N=N, sqp_iters=K, nlp_mode=1)
-        probe = max(threads, 16)
+        probe = min(B, max(threads, 16))
         tp = time.perf_counter()
         tw.closed_loop(op, x0[:probe], traj, 20, shape_id=sid[:probe], dist_step=t_dist, nthreads=threads)
         per = (time.perf_counter() - tp) / (probe * 20)
-        n = int(min(B, max(probe, args.cpu_seconds / max(per * T, 1e-9))))
-        n = max(threads, (n // threads) * threads)
+        n = int(min(B, max(probe, cpu_seconds / max(per * T, 1e-9))))
+        n = min(B, max(threads, (n // threads) * threads))
         tp = time.perf_counter()
         rc = tw.closed_loop(op, x0[:n], traj, T, shape_id=sid[:n], dist_step=t_dist, nthreads=threads)
         dt = time.perf_counter() - tp
-        result["cpu_baseline"] = {"value": n * T / dt, "unit": "lane-steps/s", "cores": threads, "kind": "port",
-                                  "cpu_model": hc["model"],
-                                  "sample": f"{n} of the {B} closed loops, all {T} steps (oracle/qsp_twin.c "
-                                            f"tw_closed_loop, OpenMP over {threads} threads, {dt:.1f} s)"}
+        out["cpu_baseline"] = {"value": n * T / dt, "unit": "lane-steps/s", "cores": threads, "kind": "port",
+                               "cpu_model": hc["model"],
+                               "sample": f"{n} of the {B} closed loops, all {T} steps (oracle/qsp_twin.c "
+                                         f"tw_closed_loop, OpenMP over {threads} threads, {dt:.1f} s)"}
         same = (np.all(r["X"][:n] == rc["X"], axis=(1, 2)) & np.all(r["U"][:n] == rc["U"], axis=(1, 2))
                 & np.all(r["status"][:n] == rc["status"], axis=1))
-        result["parity"] = {"reference": "oracle/qsp_twin.c tw_closed_loop", "lanes": int(n),
-                            "bit_identical_trajectory_lanes": int(same.sum()),
-                            "max_abs_u_err": float(np.abs(r["U"][:n] - rc["U"]).max()),
-                            "max_abs_x_err": float(np.abs(r["X"][:n] - rc["X"]).max())}
+        out["parity"] = {"reference": "oracle/qsp_twin.c tw_closed_loop", "lanes": int(n),
+                         "bit_identical_trajectory_lanes": int(same.sum()),
+                         "max_abs_u_err": float(np.abs(r["U"][:n] - rc["U"]).max()),
+                         "max_abs_x_err": float(np.abs(r["X"][:n] - rc["X"]).max())}
+    return out
+
+
+def closed_loop_bench(args):
+    """`bench.py --closed-loop`: the closed-loop measurement (closed_loop_measure) as its own line."""
+    m = closed_loop_measure(args.global_batch or CONFIG2_BATCH, args.seed, args.steps, args.cpu_seconds, args.no_cpu)
+    result = {"metric": "closed-loop controller steps/s (helper.closed_loop_matlab, main.m scenario)",
+              "value": m.pop("gpu_lane_steps_per_s"), "unit": "lane-steps/s", "n_gpus": 1, "steps": m["runs"],
+              "warmup": 1, "ms_per_step": m["ms_per_run"], "higher_is_better": True, "scaling": "strong",
+              "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+              "config": {k: m.pop(k) for k in ("workload", "batch", "N", "sqp_max_iter", "closed_loop_steps", "layout")}}
+    result.update(m)
     print(json.dumps(result), flush=True)
 
 
@@ -313,6 +320,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] (B = 4 096) side measurement")
     ap.add_argument("--no-configs4", action="store_true", help="skip the configs[4] (N = 50, B = 16 384) side measurement")
+    ap.add_argument("--no-closed-loop", action="store_true",
+                    help="skip the closed-loop side measurement (main.m's loop over 16 384 lanes, SURVEY §8(f) row 1)")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
                     help="SQP_RTI: fixed-K full steps (the BASELINE metric); SQP: the reference's merit-backtracking "
                          "SQP with KKT tolerances (sqp_iters = max_iter)")
@@ -587,6 +596,12 @@ def main():
                               "note": "host-boundary controller solves (x0 in, u0 out), 3 repeats"}
         u4_gpu = s4.get_u0()
         s4.close()
+
+    if rank == 0 and world == 1 and not args.no_closed_loop and not cfg4 and args.nlp == "SQP_RTI":
+        # SURVEY §8(f) row 1 beside the headline: main.m's closed loop, batched (bench.py --closed-loop
+        # measures it alone, over 65 536 lanes by default)
+        result["closed_loop"] = closed_loop_measure(16384, args.seed, 1, max(3.0, args.cpu_seconds / 3), args.no_cpu,
+                                                    device=gpu)
 
     if rank == 0 and world == 1 and not args.no_cpu and not cfg4:
         hc = host_cpu()

@@ -8,7 +8,7 @@ CTRS=${CTRS:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_
 for v in $VARIANTS; do
   n=$(basename $v .so)
   mkdir -p gpurun_out/abpmc/$n
-  QSP_LIB_PATH=$PWD/$v timeout -s KILL 120 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d gpurun_out/abpmc/$n/p1 -o p1 -- python3 bench.py --no-cpu --no-configs1 --no-configs4 --steps 1 --warmup 0 > gpurun_out/abpmc/$n/log 2>&1 || exit $?
+  QSP_LIB_PATH=$PWD/$v timeout -s KILL 120 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d gpurun_out/abpmc/$n/p1 -o p1 -- python3 bench.py --no-cpu --no-configs1 --no-configs4 --no-closed-loop --steps 1 --warmup 0 > gpurun_out/abpmc/$n/log 2>&1 || exit $?
   echo "== $n"
   python scripts/pmc_summary.py gpurun_out/abpmc/$n | grep -A12 "qp_step_kernel<1"
 done

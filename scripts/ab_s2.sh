@@ -10,7 +10,7 @@ for v in ${VARIANTS:-variants/*.so}; do
   n=$(basename $v .so)
   QSP_LIB_PATH=$PWD/$v timeout -k 10 300 python bench.py --config 4 --no-cpu --steps ${STEPS:-3} --warmup 1 \
     --dump-u0 gpurun_out/ab_s2/$n.c4.npz > gpurun_out/ab_s2/$n.c4.json 2> gpurun_out/ab_s2/$n.c4.err || { tail -5 gpurun_out/ab_s2/$n.c4.err; exit 1; }
-  QSP_LIB_PATH=$PWD/$v timeout -k 10 300 python bench.py --no-cpu --no-configs1 --no-configs4 --stages-per-lane 2 \
+  QSP_LIB_PATH=$PWD/$v timeout -k 10 300 python bench.py --no-cpu --no-configs1 --no-configs4 --no-closed-loop --stages-per-lane 2 \
     --steps ${STEPS:-3} --warmup 1 --dump-u0 gpurun_out/ab_s2/$n.c2.npz > gpurun_out/ab_s2/$n.c2.json 2> gpurun_out/ab_s2/$n.c2.err || { tail -5 gpurun_out/ab_s2/$n.c2.err; exit 1; }
   python - "$n" "$first" <<'EOF'
 import json, sys

@@ -16,7 +16,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 if [ -z "$SKIP_PROF" ]; then
   echo "kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/kt -o kt -- python3 bench.py --no-cpu --no-configs1 --no-configs4 --steps 3 --warmup 1 > $R/kt_bench.json 2> $R/kt_bench.err || exit $?
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/kt -o kt -- python3 bench.py --no-cpu --no-configs1 --no-configs4 --no-closed-loop --steps 3 --warmup 1 > $R/kt_bench.json 2> $R/kt_bench.err || exit $?
   python scripts/ktrace_union.py $R/kt --parts 2 > $R/kt_union.txt || exit $?
   cat $R/kt_union.txt
   echo "pmc"
