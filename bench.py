@@ -265,6 +265,69 @@ def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
     return out
 
 
+def side_rows_measure(gpu, no_cpu):
+    """SURVEY §8(f) rows 2 and 3 measured beside the headline: the shape preprocessing (PLY contour ->
+    B-spline control points and knots, PusherSliderModel.m:84-132, in the C ABI's qsp_shape_from_ply)
+    against the oracle's numpy restatement, bit for bit; and the per-lane reference generation
+    (TrajectoryGenerator.straight_line, TrajectoryGenerator.m:39-79, straight_lines_kernel) for 65 536
+    lanes x 201 samples on the device against the host mirror on a sample of lanes."""
+    import torch
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    from uclv_qs_pushing_matlab_amd.trajectory import TrajectoryGenerator
+    out = {}
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        shapes = [make_shape(n) for n in SHAPES]
+    dt = time.perf_counter() - t0
+    sp = {"shapes_per_s": reps * len(SHAPES) / dt, "note": "qsp_shape_from_ply (C++ PLY reader, float32 greedy "
+          "contour sort, knots), the four reference contours, 20 repeats"}
+    if not no_cpu:
+        from oracle.shapes_np import shape_table
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tab = shape_table(SHAPES)
+        dtn = time.perf_counter() - t0
+        same = all(int(sh.n_ctrl) == int(tab["n_ctrl"][i])
+                   and np.array_equal(np.ctypeslib.as_array(sh.ctrl)[:sh.n_ctrl], tab["ctrl"][i][:sh.n_ctrl])
+                   and np.array_equal(np.ctypeslib.as_array(sh.knots)[:sh.n_ctrl + 4], tab["knots"][i][:sh.n_ctrl + 4])
+                   for i, sh in enumerate(shapes))
+        sp.update({"cpu_shapes_per_s": reps * len(SHAPES) / dtn, "cpu_kind": "oracle/shapes_np.py (numpy)",
+                   "bit_identical_to_oracle": bool(same)})
+    out["shape_preprocessing"] = sp
+    B, T = CONFIG2_BATCH, 201
+    rng = np.random.default_rng(SEED)
+    x0 = np.stack([rng.uniform(-0.05, 0.05, B), rng.uniform(-0.05, 0.05, B), rng.uniform(-0.2, 0.2, B)], 1)
+    xf = x0 + np.stack([rng.uniform(0.02, 0.3, B), rng.uniform(-0.05, 0.05, B), rng.uniform(-0.2, 0.2, B)], 1)
+    s = OcpSolver(N=20, batch=B, device=gpu)
+    s.set_shapes([shapes[0]])
+    s.gen_straight_lines(x0, xf, 0.0, 10.0)
+    s.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        Tg = s.gen_straight_lines(x0, xf, 0.0, 10.0)
+    s.synchronize()
+    dt = (time.perf_counter() - t0) / 5
+    tab = s.get_reference_trajectories()
+    s.close()
+    rg = {"lanes_per_s": B / dt, "samples": int(Tg), "lanes": B,
+          "note": "straight_lines_kernel: one lane per thread, the quintic time law over 201 samples, host x0/xf in"}
+    n = 256
+    t0 = time.perf_counter()
+    err = 0.0
+    for i in range(n):
+        tg = TrajectoryGenerator(0.05, 0.01)
+        tg.set_target(x0[i], xf[i], 0.0, 10.0)
+        _, ref = tg.straight_line(False)
+        err = max(err, float(np.abs(tab[i, :, :3] - ref.T).max()))
+    rg.update({"host_mirror_lanes_per_s": n / (time.perf_counter() - t0), "host_mirror_sample": n,
+               "max_abs_err_vs_host_mirror": err})
+    out["reference_generation"] = rg
+    return out
+
+
 def closed_loop_bench(args):
     """`bench.py --closed-loop`: the closed-loop measurement (closed_loop_measure) as its own line."""
     m = closed_loop_measure(args.global_batch or CONFIG2_BATCH, args.seed, args.steps, args.cpu_seconds, args.no_cpu)
@@ -598,6 +661,7 @@ def main():
         s4.close()
 
     if rank == 0 and world == 1 and not args.no_closed_loop and not cfg4 and args.nlp == "SQP_RTI":
+        result["side_rows"] = side_rows_measure(gpu, args.no_cpu)
         # SURVEY §8(f) row 1 beside the headline: main.m's closed loop, batched (bench.py --closed-loop
         # measures it alone, over 65 536 lanes by default)
         result["closed_loop"] = closed_loop_measure(16384, args.seed, 1, max(3.0, args.cpu_seconds / 3), args.no_cpu,
