@@ -123,6 +123,38 @@ def host_cpu():
     return dict(nproc=os.cpu_count(), affinity_cpus=aff, model=model, threads=max(1, env or aff))
 
 
+def device_facts(dev):
+    """The GPU the line was measured on: name, compute units, and the top of the shader clock table
+    (sysfs pp_dpm_sclk of the card with this PCI bus id, when readable) -- boxes of the pool differ
+    by up to ~13 % at the same build, and this is where the difference shows."""
+    import glob
+    import torch
+    pr = torch.cuda.get_device_properties(dev)
+    out = {"name": pr.name, "gcn_arch": getattr(pr, "gcnArchName", None), "cus": pr.multi_processor_count}
+    try:
+        bus = "%04x:%02x:%02x" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        for card in glob.glob("/sys/class/drm/card*/device"):
+            if os.path.basename(os.path.realpath(card)).startswith(bus):
+                with open(os.path.join(card, "pp_dpm_sclk")) as f:
+                    mhz = [int(t.split(":")[1].strip().split("Mhz")[0].split("MHz")[0]) for t in f.read().splitlines() if ":" in t]
+                out["sclk_max_mhz"] = max(mhz)
+                for hw in glob.glob(os.path.join(card, "hwmon", "hwmon*")):
+                    for nm, key in (("power1_cap", "power_cap_w"), ("power1_cap_max", "power_cap_max_w")):
+                        pth = os.path.join(hw, nm)
+                        if os.path.exists(pth):
+                            with open(pth) as f:
+                                out[key] = int(f.read().strip()) / 1e6
+                for nm in ("product_name", "product_number"):
+                    pth = os.path.join(card, nm)
+                    if os.path.exists(pth):
+                        with open(pth) as f:
+                            out[nm] = f.read().strip()
+                break
+    except Exception:
+        pass
+    return out
+
+
 def flops_per_solve(N, K, qp_iter_total):
     return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
 
@@ -574,6 +606,7 @@ def main():
                                 "timed fork -> join" if parts > 1 else "one qp_step launch over the shard"),
                      "whole_solve_tflops": flops_solve / avg_kern_s / 1e12},
     }
+    result["device"] = device_facts(dev)
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
