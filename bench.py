@@ -159,18 +159,19 @@ def flops_per_solve(N, K, qp_iter_total):
     return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
 
 
-def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True):
+def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20):
     """The CPU restatement (port) timed on a bounded sample of the same workload (cold-start
     controller solves): the kernel-order twin (twin=True: the library's formulation on the CPU,
     OpenMP over lanes) or the literal oracle."""
     from oracle.oracle import Oracle, make_opts
     orc = Oracle(SHAPES, twin=twin)
-    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=qp_iters)
 
     def run(sl, xx=None, K_run=K, **kw):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
-        o = op if (K_run == K and not kw) else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode, **kw)
+        o = op if (K_run == K and not kw) else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode,
+                                                         **dict(dict(qp_iters=qp_iters), **kw))
         return orc.controller_solve(o, xx, traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
 
     probe = min(len(x0), max(2 * threads, 16))
@@ -185,7 +186,7 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=T
     return n, dt, r, run
 
 
-def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None):
+def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_iters=20):
     """GPU u0 vs oracle u0 on the whole CPU sample (n lanes), with the oracle's own sensitivity
     as the yardstick: a lane is chaotic when the oracle's u0 moves by > 1e-9 under
     three 1e-13 relative perturbations of x0 or when mu_stop moves 1e-10 -> 1.5e-10; parity is
@@ -204,7 +205,8 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None):
            "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
            "oracle_self_frac_le_1e-6": float(np.mean(self_dev <= 1e-6)),
            "chaotic_frac": float(np.mean(self_dev > 1e-6)),
-           "qp_rule": "HPIPM-style: mu, bound, stationarity, equality residuals < 1e-10, cap 20, stall exit, stage-0 s bound"}
+           "qp_rule": f"HPIPM-style: mu, bound, stationarity, equality residuals < 1e-10, cap {qp_iters}, stall exit, "
+                      "stage-0 s bound"}
     if gpu_dev is not None:
         # the GPU's own response to the same probes: the same share of lanes moves, largely the same
         # lanes, and the two implementations disagree almost only where one of them moves
@@ -228,10 +230,10 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None):
     return out
 
 
-def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
+def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0, qp_iters=50):
     """SURVEY §8(f) row 1, measured: helper.closed_loop_matlab as main.m runs it (helper.m:195-322;
     main.m:40-41, 105, 150-205): Hp = 10, the reference's SQP options (sqp + merit backtracking,
-    max_iter 30, tol 1e-6), time_sim 10 s (201 steps of Ts = 0.05), the 2-waypoint straight line,
+    max_iter 30, tol 1e-6; QP cap qp_iters = acados' default 50, as the MEX sets it), time_sim 10 s (201 steps of Ts = 0.05), the 2-waypoint straight line,
     no noise, no delays, the disturbance step t_dist = 15 / Ts (past the end of the run, as in main.m)
     -- batched over B lanes (x0 from the config-2 law, 4 shapes mixed per lane), the whole loop on
     the device in one host call (qsp_closed_loop_ex).  Returns lane-steps/s, the twin's closed loop
@@ -245,7 +247,7 @@ def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
     sid = (np.arange(B) % len(SHAPES)).astype(np.int32)
     traj = straight_traj()
     t_dist = int(round(15 / Ts))
-    s = OcpSolver(N=N, batch=B, sqp_iters=K, nlp_solver_type="SQP", device=device)
+    s = OcpSolver(N=N, batch=B, sqp_iters=K, qp_iters=qp_iters, nlp_solver_type="SQP", device=device)
     s.set_shapes([make_shape(n) for n in SHAPES], shape_id=sid)
     s.set_reference_trajectory(traj)
     S_layout, L_layout = s.layout()
@@ -260,7 +262,7 @@ def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
     s.close()
     el = float(np.median(times))
     out = {"workload": f"{B} closed loops of {T} steps (main.m: Hp=10, sqp + merit backtracking, max_iter 30, "
-                       "tol 1e-6, straight-line reference, no noise, no delay, t_dist past the end), 4 shapes mixed "
+                       f"tol 1e-6, QP cap {qp_iters}, straight-line reference, no noise, no delay, t_dist past the end), 4 shapes mixed "
                        "per lane, x0 from the config-2 law, whole loop on the device (qsp_closed_loop_ex, one host "
                        "call; trajectories copied back inside the timed region)",
            "gpu_lane_steps_per_s": B * T / el, "ms_per_run": el * 1e3, "runs": len(times),
@@ -274,7 +276,7 @@ def closed_loop_measure(B, seed, runs, cpu_seconds, no_cpu, device=0):
         hc = host_cpu()
         threads = hc["threads"]
         tw = Oracle(SHAPES, twin=True)
-        op = make_opts(N=N, sqp_iters=K, nlp_mode=1)
+        op = make_opts(N=N, sqp_iters=K, nlp_mode=1, qp_iters=qp_iters)
         probe = min(B, max(threads, 16))
         tp = time.perf_counter()
         tw.closed_loop(op, x0[:probe], traj, 20, shape_id=sid[:probe], dist_step=t_dist, nthreads=threads)
@@ -407,7 +409,10 @@ def main():
                          "4 = N = 50 over the curved x_finals reference")
     ap.add_argument("--N", type=int, default=0, help="horizon (0: the configuration's, 20 or 50)")
     ap.add_argument("--sqp-iters", type=int, default=50)
-    ap.add_argument("--qp-iters", type=int, default=20)
+    ap.add_argument("--qp-iters", type=int, default=20,
+                    help="QP iteration cap (the library default, 20; acados' qp_solver_iter_max default is 50: "
+                         "-2.2 %% here, but 2.3x slower at B = 4 096 where every SQP iteration waits for its slowest "
+                         "wave; DESIGN.md section 1)")
     ap.add_argument("--stages-per-lane", type=int, default=0)
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
                     help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")
@@ -614,7 +619,8 @@ def main():
                 pm = json.load(f)
             from uclv_qs_pushing_matlab_amd.build import source_digest
             same_kernel = pm.get("kernel_digest") == source_digest()
-            if same_kernel and pm.get("batch") == Bl and pm.get("N") == N and pm.get("sqp_iters") == K:
+            if (same_kernel and pm.get("batch") == Bl and pm.get("N") == N and pm.get("sqp_iters") == K
+                    and pm.get("qp_iters", 20) == args.qp_iters):
                 result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
                 result["roofline"]["traffic_source"] = ("profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE x 2 + "
                                                         "WRITE_SIZE of this kernel source (digest "
@@ -705,7 +711,8 @@ def main():
         threads = hc["threads"]
         nlp_mode = 1 if args.nlp == "SQP" else 0
         # CPU baseline: the kernel-order twin (the same algorithm and formulation, OpenMP over lanes)
-        n, dt, rt, run_t = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, nlp_mode, twin=True)
+        n, dt, rt, run_t = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, nlp_mode, twin=True,
+                                        qp_iters=args.qp_iters)
         result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
                                   "host_nproc": hc["nproc"], "host_affinity_cpus": hc["affinity_cpus"],
                                   "cpu_model": hc["model"],
@@ -715,7 +722,7 @@ def main():
         from oracle.oracle import Oracle, make_opts
         tw = Oracle(SHAPES, twin=True)
         tp = time.perf_counter()
-        rt_all = tw.controller_solve(make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode), x0, traj, 1, tw.new_warm(Bl, N),
+        rt_all = tw.controller_solve(make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=args.qp_iters), x0, traj, 1, tw.new_warm(Bl, N),
                                      shape_id=sid, nthreads=threads)
         tp = time.perf_counter() - tp
         same_u0 = np.all(u0 == rt_all["u0"], axis=1)
@@ -727,10 +734,11 @@ def main():
                             "cpu_seconds": tp}
         # the literal restatement on the first lanes, with its own sensitivity as the yardstick
         lit_s = max(3.0, args.cpu_seconds / 3)
-        nl, dtl, rl, run_l = cpu_baseline(x0, traj, sid, N, K, lit_s, threads, nlp_mode, twin=False)
+        nl, dtl, rl, run_l = cpu_baseline(x0, traj, sid, N, K, lit_s, threads, nlp_mode, twin=False,
+                                        qp_iters=args.qp_iters)
         result["cpu_literal_oracle"] = {"value": nl / dtl, "unit": "solves/s", "cores": threads,
                                         "sample": f"{nl} lanes (oracle/qsp_oracle.c: full basis sum, forward AD)"}
-        pl = parity_leg(u0, x0, traj, sid, N, K, nl, rl, run_l, args.nlp, gpu_dev)
+        pl = parity_leg(u0, x0, traj, sid, N, K, nl, rl, run_l, args.nlp, gpu_dev, qp_iters=args.qp_iters)
         # the GPU equals the twin, so its differences from the literal restatement are the two CPU
         # formulations' differences (span-based de Boor + hand-derived Jacobian vs basis sum + AD)
         pl["twin_vs_literal_max_abs_u0_err"] = float(np.abs(rt_all["u0"][:nl] - rl["u0"]).max())
@@ -739,7 +747,7 @@ def main():
             # configs[1] on the CPU in full (the twin: rate and bit-for-bit parity of every lane)
             x1, traj1, sid1 = config1_inputs(N)
             tc = time.perf_counter()
-            r1 = tw.controller_solve(make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode), x1, traj1, 1,
+            r1 = tw.controller_solve(make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=args.qp_iters), x1, traj1, 1,
                                      tw.new_warm(len(x1), N), shape_id=sid1, nthreads=threads)
             dtc = time.perf_counter() - tc
             result["configs1"].update({"cpu_solves_per_s": len(x1) / dtc, "cpu_seconds": dtc, "cpu_threads": threads,
@@ -749,7 +757,7 @@ def main():
         if "configs4" in result:
             # configs[4]: every lane against the twin (N = 50: the two-stages-per-lane layout's order)
             t4c = time.perf_counter()
-            r4 = tw.controller_solve(make_opts(N=50, sqp_iters=K), x4, traj4, idx4b, tw.new_warm(len(x4), 50),
+            r4 = tw.controller_solve(make_opts(N=50, sqp_iters=K, qp_iters=args.qp_iters), x4, traj4, idx4b, tw.new_warm(len(x4), 50),
                                      shape_id=sid4, nthreads=threads)
             result["configs4"].update({"lanes": int(len(x4)), "cpu_seconds": time.perf_counter() - t4c,
                                        "bit_identical_u0_lanes": int(np.sum(np.all(u4_gpu == r4["u0"], axis=1))),

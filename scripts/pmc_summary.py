@@ -24,6 +24,7 @@ ap.add_argument("--kernel", default="qp_step_kernel")
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--N", type=int, default=20)
 ap.add_argument("--sqp-iters", type=int, default=50)
+ap.add_argument("--qp-iters", type=int, default=20, help="QP iteration cap of the profiled solves (bench.py default)")
 ap.add_argument("--parts", type=int, default=2, help="stream parts of the profiled solves (bench.py layout)")
 args = ap.parse_args()
 
@@ -51,7 +52,7 @@ if args.json:
     write = sum(tot[k]["WRITE_SIZE"] for k in ks) / (sum(len(ndisp[k]["WRITE_SIZE"]) for k in ks) / args.parts)
     rd, wr = fetch * 1024 * 2, write * 1024
     out = {"kernel": args.kernel, "batch": args.batch, "N": args.N, "sqp_iters": args.sqp_iters,
-           "stream_parts": args.parts, "per": "SQP iteration over the whole batch (= bench roofline launch)",
+           "qp_iters": args.qp_iters, "stream_parts": args.parts, "per": "SQP iteration over the whole batch (= bench roofline launch)",
            "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
            "raw_FETCH_SIZE_KiB": fetch, "raw_WRITE_SIZE_KiB": write,
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count), WRITE_SIZE KiB x 1024",
