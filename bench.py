@@ -198,12 +198,22 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_ite
         self_dev = np.maximum(self_dev, np.abs(run(slice(0, n), x0[:n] * (1 + sgn * f * 1e-13))["u0"] - u0_ref).max(1))
     mu_dev = np.abs(run(slice(0, n), mu_stop=1.5e-10)["u0"] - u0_ref).max(1)
     nonchaotic = (self_dev < 1e-9) & (mu_dev < 1e-9)
+    # the model probe (oracle/or_opts.h): the linearisation's outputs moved by +-1e-14 of their scale,
+    # the size by which the literal and the kernel-order formulations differ
+    mod_dev = np.zeros(n)
+    for seed in (1, 2):
+        mod_dev = np.maximum(mod_dev, np.abs(run(slice(0, n), model_probe=1e-14, probe_seed=seed)["u0"] - u0_ref).max(1))
     out = {"lanes": int(n), "max_abs_u0_err": float(d.max()),
            "nonchaotic_lanes": int(nonchaotic.sum()),
            "max_abs_u0_err_nonchaotic": float(d[nonchaotic].max()) if nonchaotic.any() else None,
            "frac_nonchaotic_err_le_1e-6": float(np.mean(d[nonchaotic] <= 1e-6)) if nonchaotic.any() else None,
            "frac_lanes_err_le_1e-6": float(np.mean(d <= 1e-6)),
            "oracle_self_frac_le_1e-6": float(np.mean(self_dev <= 1e-6)),
+           "lanes_err_gt_1e-6": int(np.sum(d > 1e-6)),
+           "lanes_err_gt_1e-6_moving_under_x0_or_model_probes": int(np.sum((d > 1e-6) & ((self_dev > 1e-6) | (mod_dev > 1e-6)))),
+           "lanes_stable_under_all_probes": int(np.sum(nonchaotic & (mod_dev < 1e-9))),
+           "max_abs_u0_err_stable_under_all_probes": float(d[nonchaotic & (mod_dev < 1e-9)].max())
+                                                     if np.any(nonchaotic & (mod_dev < 1e-9)) else None,
            "chaotic_frac": float(np.mean(self_dev > 1e-6)),
            "qp_rule": f"HPIPM-style: mu, bound, stationarity, equality residuals < 1e-10, cap {qp_iters}, stall exit, "
                       "stage-0 s bound"}
@@ -226,7 +236,8 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_ite
         out["chaotic_frac_first"] = {"lanes": int(m), "this_rule": float(np.mean(self_dev[:m] > 1e-6)),
                                      "round1_rule": float(np.mean(dev > 1e-6))}
     out["note"] = ("u0_ref = CPU oracle (acados parity unpinned); nonchaotic = the oracle itself moves < 1e-9 under "
-                   "three 1e-13 relative x0 perturbations and mu_stop 1.5e-10")
+                   "three 1e-13 relative x0 perturbations and mu_stop 1.5e-10; model probes = the oracle with its "
+                   "linearisation moved by +-1e-14 of scale (two sign patterns)")
     return out
 
 

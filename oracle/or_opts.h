@@ -48,6 +48,15 @@ typedef struct {
     int32_t stages_per_lane; /* twin only: the device layout S whose arithmetic order it follows (0: the
                                 library's choice, 1 for N + 1 <= 32 or nlp_mode 1, else 2) */
     double qp_mu_max;   /* divergence exit: mu >= qp_mu_max (or non-finite) is a QP failure (status 4) */
+    /* literal restatement only (the twin ignores it): the model probe.  Every entry of each output
+     * of the linearisation (x+, A, B of rk4_sens) moves by +- model_probe x that array's largest
+     * entry, the sign hashed from probe_seed, the stage's inputs and the entry -- a perturbation of
+     * the model of the size by which the two formulations differ (measured: up to 1.6e-13 of the
+     * scale in A, 5.5e-14 in B, 1e-14 in x+), to tell lanes whose u0 depends on those last digits
+     * of the model from the others.  0: off. */
+    double model_probe;
+    int32_t probe_seed;
+    int32_t pad2_;
 } or_opts;
 
 #endif

@@ -245,6 +245,38 @@ static double v_bound(const or_shape *sh, const or_opts *o, double s)
 static const double RK_A[4] = {0.0, 0.5, 0.5, 1.0};
 static const double RK_B[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
 
+/* The model probe (or_opts.model_probe): set by the solve entry points before their parallel
+ * region, read-only inside it. */
+static double g_probe_eps = 0.0;
+static uint64_t g_probe_seed = 0;
+
+static inline uint64_t mix64(uint64_t z)
+{
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+static void probe_outputs(const double x[4], const double u[2], double xn[4], double A[16], double B[8])
+{
+    uint64_t h = mix64(g_probe_seed);
+    for (int i = 0; i < 4; ++i) { uint64_t b; memcpy(&b, &x[i], 8); h = mix64(h ^ b); }
+    for (int i = 0; i < 2; ++i) { uint64_t b; memcpy(&b, &u[i], 8); h = mix64(h ^ b); }
+    double *out[3] = {xn, A, B};
+    const int len[3] = {4, 16, 8};
+    int e = 0;
+    for (int a = 0; a < 3; ++a) {
+        double scale = 0.0;   /* the array's largest entry: differences between formulations are
+                                 absolute at that scale, not relative to each (possibly tiny) entry */
+        for (int i = 0; i < len[a]; ++i) scale = fmax(scale, fabs(out[a][i]));
+        for (int i = 0; i < len[a]; ++i, ++e) {
+            const uint64_t r = mix64(h + (uint64_t)e);
+            out[a][i] += ((r & 1) ? g_probe_eps : -g_probe_eps) * scale;
+        }
+    }
+}
+
 /* x+ = phi(x,u) and A = dphi/dx (4x4), B = dphi/du (4x2), row-major */
 static void rk4_sens(const or_shape *sh, double h, const double x[4], const double u[2],
                      double xn[4], double A[16], double B[8])
@@ -286,6 +318,7 @@ static void rk4_sens(const or_shape *sh, double h, const double x[4], const doub
         for (int j = 0; j < 4; ++j) A[i * 4 + j] = S[j];
         for (int j = 0; j < 2; ++j) B[i * 2 + j] = S[4 + j];
     }
+    if (g_probe_eps != 0.0) probe_outputs(x, u, xn, A, B);
 }
 
 /* ================================================================ QP (IPM) */
@@ -807,6 +840,7 @@ int or_rk4(const int32_t *n_ctrl, const double *ctrl, const double *knots, const
            int max_ctrl, int32_t n, const int32_t *shape_id, double h, const double *x, const double *u,
            double *xn, double *A, double *B)
 {
+    g_probe_eps = 0.0;
     #pragma omp parallel for schedule(static)
     for (int32_t i = 0; i < n; ++i) {
         or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
@@ -870,6 +904,8 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
                  double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
                  double *cost, int nthreads, int32_t *qp_capped, int32_t *qp_stalled)
 {
+    g_probe_eps = o->model_probe;
+    g_probe_seed = (uint64_t)(uint32_t)o->probe_seed;
     int N = o->N;
     if (N > OR_MAX_N) return -1;
 #ifdef _OPENMP
@@ -989,6 +1025,8 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                         double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads,
                         int32_t *qp_capped, int32_t delay_cols, int32_t *qp_stalled)
 {
+    g_probe_eps = o->model_probe;
+    g_probe_seed = (uint64_t)(uint32_t)o->probe_seed;
     int N = o->N;
     if (N > OR_MAX_N) return -1;
 #ifdef _OPENMP
@@ -1068,6 +1106,8 @@ int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
                    int32_t delay_cols, int32_t plant_delay_cols, int32_t dist_step, const double *dist_amp,
                    const double *xwidth, double *Xtraj, double *Xsim, double *Utraj, int32_t *Straj, int nthreads)
 {
+    g_probe_eps = o->model_probe;
+    g_probe_seed = (uint64_t)(uint32_t)o->probe_seed;
     int N = o->N;
     if (N > OR_MAX_N || delay_cols < 0 || plant_delay_cols < 0 || delay_cols > 1024 || plant_delay_cols > 1024) return -1;
 #ifdef _OPENMP

@@ -389,3 +389,24 @@ def test_reference_table_prefix_and_closed_loop_composition(oracle):
     # original columns, so it equals the undelayed first step
     rd = oracle.closed_loop(op, x0, traj, 2, shape_id=sid, delay_cols=2)
     np.testing.assert_array_equal(rd["U"][:, 0], r["U"][:, 0])
+
+
+def test_model_probe(oracle):
+    """The model probe (or_opts.model_probe, used by bench.py's parity leg): off by default and at 0,
+    deterministic per seed whatever the thread count, and a perturbation of the model's size only
+    (u0 of a one-iteration solve moves by at most ~1e-9)."""
+    N, nb = 20, 24
+    x0 = config2_x0(nb, 41)
+    traj = straight_traj()
+
+    def run(threads=4, **kw):
+        return oracle.controller_solve(make_opts(N=N, sqp_iters=1, **kw), x0, traj, 1, oracle.new_warm(nb, N),
+                                       nthreads=threads)["u0"]
+    base = run()
+    assert np.array_equal(run(model_probe=0.0, probe_seed=7), base)
+    p1 = run(model_probe=1e-14, probe_seed=1)
+    assert not np.array_equal(p1, base)
+    assert np.abs(p1 - base).max() < 1e-9
+    assert np.array_equal(run(threads=1, model_probe=1e-14, probe_seed=1), p1)
+    assert not np.array_equal(run(model_probe=1e-14, probe_seed=2), p1)
+    assert np.array_equal(run(), base)      # the probe does not leak into the next solve
