@@ -100,7 +100,8 @@ def controller_pair(twin, N, B, x0, traj, sid, idx, K=50, steps=1, **kw):
     s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI", **kw)
     s.set_shape_ids(sid)
     s.set_reference_trajectory(traj)
-    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp, qp_iters=kw.get("qp_iters", 20), qp_mu_max=kw.get("qp_mu_max", 1e100))
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp, qp_iters=kw.get("qp_iters", 20), qp_mu_max=kw.get("qp_mu_max", 1e100),
+                   stages_per_lane=kw.get("stages_per_lane", 0))
     warm = twin.new_warm(B, N)
     for step in range(steps):
         u = s.controller_solve(x0, idx + step)
@@ -227,3 +228,28 @@ def test_qp_divergence_exit_bit_identical(twin, mu_max):
         assert np.all(r["status"] == 4) and np.all(r["iters"] == 0)
     else:
         assert 0 < np.sum(r["status"] == 4) < 200
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("N,S", [(1, 1), (2, 1), (2, 2), (31, 1), (32, 0), (32, 1), (63, 1), (63, 2), (100, 2), (127, 2)])
+def test_horizons_and_layouts_bit_identical(twin, monkeypatch, N, S, fused):
+    """Every lane layout the library accepts, at its edges: one stage per lane from N = 1 (32 instances
+    per wave) to N = 63 (one instance filling the wave), two stages per lane up to N = 127; the auto
+    choice at N = 32 (two stages per lane); 97 lanes (a partly filled last wave), mixed shapes, both the
+    per-iteration launches and the fused small-batch loop (QSP_FUSED_LOOP)."""
+    from bench import SEED, make_inputs
+    monkeypatch.setenv("QSP_FUSED_LOOP", fused)
+    nb = 97
+    x0, _, _, sid, traj = make_inputs(nb, N, SEED + N)
+    controller_pair(twin, N, nb, x0, traj, sid, 1, K=8, stages_per_lane=S)
+
+
+def test_main_m_controller_and_acados_qp_cap_bit_identical(twin):
+    """main.m's own controller (Hp = 10, sqp + merit backtracking, max_iter 30, NMPC_controller.m:271-276)
+    at acados' QP iteration cap (qp_solver_iter_max 50, as the MEX sets it), three controller steps; and
+    the fixed-K workload at that cap."""
+    from bench import SEED, make_inputs
+    x0, _, _, sid, traj = make_inputs(2048, 10, SEED + 10)
+    controller_pair(twin, 10, 2048, x0, traj, sid, 1, K=30, steps=3, nlp_mode=1, qp_iters=50)
+    x0, _, _, sid, traj = make_inputs(2048, 20, SEED + 20)
+    controller_pair(twin, 20, 2048, x0, traj, sid, 1, qp_iters=50)
