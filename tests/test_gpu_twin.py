@@ -253,3 +253,42 @@ def test_main_m_controller_and_acados_qp_cap_bit_identical(twin):
     controller_pair(twin, 10, 2048, x0, traj, sid, 1, K=30, steps=3, nlp_mode=1, qp_iters=50)
     x0, _, _, sid, traj = make_inputs(2048, 20, SEED + 20)
     controller_pair(twin, 20, 2048, x0, traj, sid, 1, qp_iters=50)
+
+
+def test_non_default_parameters_bit_identical(twin):
+    """Every tunable of the OCP and the solver away from its default (NMPC_controller.m
+    update_cost_function :153-164, update_constraints :122-142, the ctor's v_alpha / d_v_bound /
+    t_angle0 :98-100 and input bounds :23-26, Ts, the stage-cost scaling, the IPM's parameters), two
+    controller steps: the device and the twin read them the same way."""
+    from oracle.oracle import make_opts
+    from bench import SEED, make_inputs
+    N, nb, K = 16, 1024, 12
+    W = np.array([2.0, 0.5, 3e-3, 1e-4, 2e-3, 5e-4])
+    We = np.array([1e5, 3e5, 10.0, 1.0])
+    lh, uh = np.array([-0.05, 0.0, -0.04]), np.array([0.02, 0.025, 0.04])
+    ctrl = dict(v_alpha=0.8, d_v=0.001, t_angle0=2.5, u_n_lb=0.001, u_t_ub=0.04)
+    ipm = dict(mu0=0.5, t_min=2e-2, frac=0.99, sigma_min=0.05, mu_stop=1e-9, res_stop=1e-9, qp_tol_stat=1e-9,
+               qp_tol_eq=1e-9, qp_stall_iters=4, qp_stall_alpha=5e-4)
+    x0, _, _, sid, traj = make_inputs(nb, N, SEED + 99)
+    x0[:, 3] = np.clip(x0[:, 3], lh[0] + 1e-3, uh[0] - 1e-3)
+    s = solver(N, nb, sqp_iters=K, qp_iters=25, Ts=0.04, cost_scale_Ts=False, stage0_s_bound=False, **ipm)
+    s.set_shape_ids(sid)
+    s.set("cost_W", np.diag(W))
+    s.set("cost_W", np.diag(We), stage=N)
+    s.set("constr_lh", lh)
+    s.set("constr_uh", uh)
+    s.set_ctrl_params(ctrl["v_alpha"], ctrl["d_v"], ctrl["t_angle0"], ctrl["u_n_lb"], ctrl["u_t_ub"])
+    s.set_reference_trajectory(traj)
+    op = make_opts(N=N, sqp_iters=K, qp_iters=25, Ts=0.04, tau=1.0, W=tuple(W), We=tuple(We), lh=tuple(lh),
+                   uh=tuple(uh), stage0_s_bound=0, **ctrl, **ipm)
+    warm = twin.new_warm(nb, N)
+    for step in range(2):
+        u = s.controller_solve(x0, 1 + step)
+        r = twin.controller_solve(op, x0, traj, 1 + step, warm, shape_id=sid)
+        same(u, r["u0"], f"u0 (step {step})")
+        for f in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
+            same(s.get(f), r[{"sqp_iter": "iters"}.get(f, f)], f"{f} (step {step})")
+        same(s.get("x"), warm["X"], f"warm X (step {step})")
+        same(s.get_cost(), r["cost"], f"cost (step {step})")
+    s.close()
+    assert np.mean(r["status"] == 0) > 0.9
