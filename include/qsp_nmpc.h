@@ -179,6 +179,11 @@ int qsp_get_qp_capped(qsp_solver* s, int32_t* capped /* B */);
 /* QPs of the last solve stopped by the stall exit (qp_stall_iters steps below qp_stall_alpha;
  * their last iterate is used as at the cap): B counts */
 int qsp_get_qp_stalled(qsp_solver* s, int32_t* stalled /* B */);
+/* nlp_mode 1 only (else QSP_ERR_STATE): the NLP's KKT residuals of the last test each instance
+ * evaluated -- acados' statistics res_stat, res_eq, res_ineq, res_comp (max norms; ocp_nlp_res of
+ * the SQP with nlp_solver_tol_* at NMPC_controller.m:275-276).  For status 0 that is the test that
+ * passed; for status 2 the test before the last QP; zeros for an instance that never iterated. */
+int qsp_get_residuals(qsp_solver* s, double* res /* B x 4 */);
 int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
 /* dims of the handle (outputs of a MEX/FFI layer are sized from these, never from caller input) */
 int qsp_get_dims(const qsp_solver* s, int32_t* N, int32_t* B);

@@ -146,6 +146,9 @@ static double mat_mod(double a, double b)
 
 /* ================================================================ dynamics */
 /* f(x,u) and J = d f / d(x,u) (4 x 6, row-major) — PusherSliderModel.m:503-603 */
+/* motion-cone modes of the dynamics evaluations since the last reset, base 4 (diagnostics only) */
+static __thread int g_mode_code = 0;
+
 static void dynamics(const or_shape *sh, const double x[4], const double u[2], double f[4], double *J)
 {
     dual X[4], U[2];
@@ -217,6 +220,7 @@ static void dynamics(const or_shape *sh, const double x[4], const double u[2], d
     /* indicator blend (:587-589); comparisons with NaN are false */
     dual ist = dmul(dind(rho.v >= gr.v), dind(rho.v <= gl.v));
     dual isl = dind(rho.v > gl.v), isr = dind(rho.v < gr.v);
+    g_mode_code = g_mode_code * 4 + (ist.v != 0.0 ? 0 : (isl.v != 0.0 ? 1 : (isr.v != 0.0 ? 2 : 3)));
     for (int r = 0; r < 4; ++r) {
         dual v = dadd(dadd(dmul(ist, st[r]), dmul(isl, sl[r])), dmul(isr, sr[r]));
         f[r] = v.v;
@@ -340,6 +344,13 @@ typedef struct {
     double *lam;  /* N x 3 x 2 (lo, hi) */
     double *t;    /* N x 3 x 2 */
 } or_qp_sol;
+
+/* Experiments on the merit SQP (tests/tools/kkt_breakdown.py; 0 = the reference's algorithm):
+ *   1 full-step multipliers (PI, LAM = the QP's; acados full_step_dual),
+ *   2 the QP's u-bound multipliers recovered from its u-stationarity (exact QP duals),
+ *   4 no minimum step: backtrack down to 1e-12 instead of accepting the step at ls_alpha_min. */
+static int g_exp = 0;
+void or_set_experiment(int flags) { g_exp = flags; }
 
 static void inv2(const double R[4], double Ri[4])
 {
@@ -490,8 +501,10 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
          * residuals r0, rg0, rb0 times their common scale prod(1 - alpha) -- tested as
          * prod < min(tol / r) (x / 0 = inf: a residual that starts at zero never binds) */
         if (!(mu >= o->mu_stop) && !(rscale >= rs_stop)) { converged = 1; break; }
-        if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
+        /* the stall exit is tested before the cap, as the kernel's qp_ipm does, so that a QP stalled at
+         * the cap counts as stalled in both */
         if (o->qp_stall_iters > 0 && stall >= o->qp_stall_iters) { stalled = 1; break; }   /* as at the cap */
+        if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
@@ -588,6 +601,18 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         memcpy(pi, np, sizeof pi);
         memcpy(sol->pi + 4 * (k - 1), pi, sizeof pi);
     }
+    if (g_exp & 2) {
+        for (int k = 0; k < N; ++k) {
+            const double *B = qp->B + 8 * k, *pk = sol->pi + 4 * k;
+            for (int i = 0; i < 2; ++i) {
+                double r = qp->H[6 * k + 4 + i] * sol->du[2 * k + i] + qp->g[6 * k + 4 + i];
+                for (int j = 0; j < 4; ++j) r += B[j * 2 + i] * pk[j];
+                const int q = (k * 3 + 1 + i) * 2;
+                lam[q + 1] = -r > 0.0 ? -r : 0.0;
+                lam[q] = r > 0.0 ? r : 0.0;
+            }
+        }
+    }
     for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(sol->dx[q])) return 1;
     for (int q = 0; q < 2 * N; ++q) if (!isfinite(sol->du[q])) return 1;
     if (infeasible) return 3;
@@ -608,7 +633,21 @@ typedef struct {
     int qp_total;
     int qp_capped;   /* QPs of this solve stopped by the iteration cap */
     int qp_stalled;  /* ... by the stall exit */
+    int mode[OR_MAX_N];  /* motion-cone modes of the stages' RK4 evaluations (diagnostics) */
+    double kkt[18];  /* diagnostics of the last NLP KKT test (nlp_mode 1): see or_set_kkt_diag */
 } or_ws;
+
+/* KKT diagnostics (nlp_mode 1), per lane 18 doubles: the residuals of the last KKT test the SQP
+ * evaluated -- u-stationarity, x-stationarity (stages 1..N-1), terminal stationarity, equality,
+ * inequality, complementarity -- then the SQP iteration of that test, the last line-search
+ * step length, that line search's directional derivative, merit at alpha = 0 and at the last step
+ * tried, the number of line searches that ended at ls_alpha_min; for the last QP its exit code,
+ * the term sum r_u' du of its u-stationarity residual r_u, -d'Hd, and sum pi'b - nu|b|; the number
+ * of stages whose motion-cone modes (at the four RK4 evaluations) changed between the last two
+ * linearisations, and over all linearisations from SQP iteration 10 on.  NULL: off. */
+static double *g_kkt_diag = NULL;
+void or_set_kkt_diag(double *buf) { g_kkt_diag = buf; }
+
 
 static double ocp_cost(const or_opts *o, int N, const double *X, const double *U, const double *yref, const double *yref_e)
 {
@@ -668,6 +707,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
     memset(nu, 0, sizeof(double) * 4 * N);
     memset(eta, 0, sizeof(double) * 6 * N);
     int it;
+    memset(ws->kkt, 0, sizeof ws->kkt);
     if (o->nlp_mode == 1) status = 2;
     /* stage-0 s bound: s_0 = x0's s is fixed in every QP; outside [lh_s, uh_s] all of them are
      * infeasible and the solve stops before its first iteration (status 4, ACADOS_QP_FAILURE) */
@@ -677,9 +717,16 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         return 4;
     }
     for (it = 0; it < o->sqp_iters; ++it) {
+        ws->kkt[16] = 0.0;
         for (int k = 0; k < N; ++k) {
             double xn[4];
+            g_mode_code = 0;
             rk4_sens(sh, o->Ts, X + 4 * k, U + 2 * k, xn, ws->A + 16 * k, ws->B + 8 * k);
+            if (it > 0 && g_mode_code != ws->mode[k]) {
+                if (it >= 10) ws->kkt[17] += 1.0;
+                ws->kkt[16] += 1.0;
+            }
+            ws->mode[k] = g_mode_code;
             for (int i = 0; i < 4; ++i) ws->b[4 * k + i] = xn[i] - X[4 * (k + 1) + i];
             for (int i = 0; i < 4; ++i) {
                 ws->H[6 * k + i] = o->tau * o->W[i];
@@ -703,7 +750,8 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         }
         if (o->nlp_mode == 1) {
             /* KKT residuals of the NLP at the current iterate */
-            double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0;
+            ws->kkt[2] = 0.0;
+            double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0, r_u = 0.0, r_x = 0.0;
             for (int k = 0; k < N; ++k) {
                 const double *A = ws->A + 16 * k, *B = ws->B + 8 * k, *pk = PI + 4 * k;
                 for (int i = 0; i < 2; ++i) {
@@ -711,6 +759,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                     for (int j = 0; j < 4; ++j) r += B[j * 2 + i] * pk[j];
                     r += LAM[(3 * k + 1 + i) * 2 + 1] - LAM[(3 * k + 1 + i) * 2 + 0];
                     if (fabs(r) > r_stat) r_stat = fabs(r);
+                    if (fabs(r) > r_u) r_u = fabs(r);
                 }
                 if (k >= 1) {
                     for (int i = 0; i < 4; ++i) {
@@ -718,6 +767,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                         for (int j = 0; j < 4; ++j) r += A[j * 4 + i] * pk[j];
                         if (i == 3) r += LAM[(3 * k) * 2 + 1] - LAM[(3 * k) * 2 + 0];
                         if (fabs(r) > r_stat) r_stat = fabs(r);
+                        if (fabs(r) > r_x) r_x = fabs(r);
                     }
                 }
                 for (int i = 0; i < 4; ++i) if (fabs(ws->b[4 * k + i]) > r_eq) r_eq = fabs(ws->b[4 * k + i]);
@@ -733,7 +783,10 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
             for (int i = 0; i < 4; ++i) {
                 double r = ws->g[6 * N + i] - PI[4 * (N - 1) + i];
                 if (fabs(r) > r_stat) r_stat = fabs(r);
+                if (fabs(r) > ws->kkt[2]) ws->kkt[2] = fabs(r);
             }
+            ws->kkt[0] = r_u; ws->kkt[1] = r_x; ws->kkt[3] = r_eq; ws->kkt[4] = r_ineq; ws->kkt[5] = r_comp;
+            ws->kkt[6] = it;
             if (r_stat < o->tol_stat && r_eq < o->tol_eq && r_ineq < o->tol_ineq && r_comp < o->tol_comp) {
                 status = 0;
                 break;
@@ -773,20 +826,44 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 }
             }
             for (int i = 0; i < 4; ++i) dphi += ws->g[6 * N + i] * ws->dx[4 * N + i];
+            ws->kkt[8] = dphi;
+            ws->kkt[9] = phi0;
+            {
+                double ru = 0.0, dhd = 0.0, pb = 0.0;
+                for (int k = 0; k < N; ++k) {
+                    const double *Bk = ws->B + 8 * k, *pk = ws->pi + 4 * k;
+                    for (int i = 0; i < 2; ++i) {
+                        double r = ws->H[6 * k + 4 + i] * ws->du[2 * k + i] + ws->g[6 * k + 4 + i];
+                        for (int j = 0; j < 4; ++j) r += Bk[j * 2 + i] * pk[j];
+                        r += ws->lam[(k * 3 + 1 + i) * 2 + 1] - ws->lam[(k * 3 + 1 + i) * 2 + 0];
+                        ru += r * ws->du[2 * k + i];
+                        dhd -= ws->H[6 * k + 4 + i] * ws->du[2 * k + i] * ws->du[2 * k + i];
+                    }
+                    for (int i = 0; i < 4; ++i) {
+                        dhd -= ws->H[6 * k + i] * ws->dx[4 * k + i] * ws->dx[4 * k + i];
+                        pb += pk[i] * ws->b[4 * k + i] - nu[4 * k + i] * fabs(ws->b[4 * k + i]);
+                    }
+                }
+                for (int i = 0; i < 4; ++i) dhd -= ws->H[6 * N + i] * ws->dx[4 * N + i] * ws->dx[4 * N + i];
+                ws->kkt[12] = qst; ws->kkt[13] = ru; ws->kkt[14] = dhd; ws->kkt[15] = pb;
+            }
             for (;;) {
                 for (int q = 0; q < 4 * (N + 1); ++q) Xt[q] = X[q] + alpha * ws->dx[q];
                 for (int q = 0; q < 2 * N; ++q) Ut[q] = U[q] + alpha * ws->du[q];
                 double phi = merit_eval(sh, o, Xt, Ut, yref, yref_e, nu, eta);
+                ws->kkt[10] = phi;
                 if (phi <= phi0 + o->ls_eps * alpha * dphi) break;
                 double an = alpha * o->ls_alpha_red;
-                if (an < o->ls_alpha_min) break;   /* accept the last step tried */
+                if (an < ((g_exp & 4) ? 1e-12 : o->ls_alpha_min)) { ws->kkt[11] += 1.0; break; }   /* accept the last step tried */
                 alpha = an;
             }
+            ws->kkt[7] = alpha;
         }
         for (int q = 0; q < 4 * (N + 1); ++q) X[q] += alpha * ws->dx[q];
         for (int q = 0; q < 2 * N; ++q) U[q] += alpha * ws->du[q];
-        for (int q = 0; q < 4 * N; ++q) PI[q] += alpha * (ws->pi[q] - PI[q]);
-        for (int q = 0; q < 6 * N; ++q) LAM[q] += alpha * (ws->lam[q] - LAM[q]);
+        const double ad = (g_exp & 1) ? 1.0 : alpha;
+        for (int q = 0; q < 4 * N; ++q) PI[q] += ad * (ws->pi[q] - PI[q]);
+        for (int q = 0; q < 6 * N; ++q) LAM[q] += ad * (ws->lam[q] - LAM[q]);
     }
     if (iters) *iters = it;
     if (lam_out) memcpy(lam_out, LAM, sizeof(double) * 6 * N);
@@ -926,6 +1003,7 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
             if (qp_iter) qp_iter[i] = ws->qp_total;
             if (qp_capped) qp_capped[i] = ws->qp_capped;
             if (qp_stalled) qp_stalled[i] = ws->qp_stalled;
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)18 * i, ws->kkt, sizeof ws->kkt);
             cost[i] = ocp_cost(o, N, Xi, Ui, yr, ye);
         }
         free(ws);
@@ -1042,6 +1120,7 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
                                         Xw + (size_t)i * 4 * (N + 1), Uw + (size_t)i * 2 * N, PIw + (size_t)i * 4 * N,
                                         warm_valid + i, u0 + 2 * i, iters ? iters + i : NULL, qp_iter ? qp_iter + i : NULL,
                                         qp_capped ? qp_capped + i : NULL, cost + i, ws, qp_stalled ? qp_stalled + i : NULL);
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)18 * i, ws->kkt, sizeof ws->kkt);
         }
         free(ws);
     }

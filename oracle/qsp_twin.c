@@ -863,7 +863,14 @@ typedef struct {
     tw_stage st[TW_MAX_SLOTS];
     double nlpPI[TW_MAX_N * 4], LAM[TW_MAX_N * 6], NU[TW_MAX_N * 4], ETA[TW_MAX_N * 6];
     double qPI[TW_MAX_N * 4];
+    double kkt[8];   /* diagnostics of the last NLP KKT test (nlp_mode 1): see tw_set_kkt_diag */
 } tw_ws;
+
+/* KKT diagnostics (nlp_mode 1), per lane 8 doubles, as or_set_kkt_diag: u-, x- and terminal
+ * stationarity, equality, inequality, complementarity residuals of the last KKT test, its SQP
+ * iteration, the last line-search step length.  NULL: off. */
+static double *g_kkt_diag = NULL;
+void tw_set_kkt_diag(double *buf) { g_kkt_diag = buf; }
 
 /* stage data of slot k from the SQP iterate (qp_step_kernel's LIN block) */
 static void load_stage(const tw_par *p, const tw_shape *sh, tw_stage *s, int k, const double *X, const double *U,
@@ -894,10 +901,10 @@ static void load_stage(const tw_par *p, const tw_shape *sh, tw_stage *s, int k, 
 }
 
 /* nlp_converged: KKT residuals of the NLP iterate against tol_* (nlp_mode 1) */
-static int nlp_converged(const tw_par *p, const tw_stage *st, const double *PI, const double *LAM)
+static int nlp_converged(const tw_par *p, const tw_stage *st, const double *PI, const double *LAM, double *kkt)
 {
     const int N = p->N;
-    double rs = 0.0, re = 0.0, ri = 0.0, rc = 0.0;
+    double rs = 0.0, re = 0.0, ri = 0.0, rc = 0.0, ru = 0.0, rx = 0.0, rt = 0.0;
     for (int k = 0; k <= N; ++k) {
         const tw_stage *s = st + k;
         const double zero[6] = {0, 0, 0, 0, 0, 0};
@@ -909,6 +916,7 @@ static int nlp_converged(const tw_par *p, const tw_stage *st, const double *PI, 
                 const double r = (s->g[4 + i] + qfma(B[6 + i], PIk[3], qfma(B[4 + i], PIk[2], qfma(B[2 + i], PIk[1], B[i] * PIk[0])))) +
                                  (LAMk[2 * (1 + i) + 1] - LAMk[2 * (1 + i)]);
                 rs = fmax(rs, fabs(r));
+                ru = fmax(ru, fabs(r));
             }
             if (k >= 1) {
                 const double at[4] = {PIk[0], PIk[1], qfma(a[2], PIk[1], a[0] * PIk[0]) + PIk[2],
@@ -917,6 +925,7 @@ static int nlp_converged(const tw_par *p, const tw_stage *st, const double *PI, 
                     double r = s->g[i] - PIp[i] + at[i];
                     if (i == 3) r += LAMk[1] - LAMk[0];
                     rs = fmax(rs, fabs(r));
+                    rx = fmax(rx, fabs(r));
                 }
             }
             for (int i = 0; i < 4; ++i) re = fmax(re, fabs(s->bb[i]));
@@ -928,8 +937,10 @@ static int nlp_converged(const tw_par *p, const tw_stage *st, const double *PI, 
             }
         } else {
             for (int i = 0; i < 4; ++i) rs = fmax(rs, fabs(s->g[i] - PIp[i]));
+            for (int i = 0; i < 4; ++i) rt = fmax(rt, fabs(s->g[i] - PIp[i]));
         }
     }
+    kkt[0] = ru; kkt[1] = rx; kkt[2] = rt; kkt[3] = re; kkt[4] = ri; kkt[5] = rc;
     return rs < p->tol_stat && re < p->tol_eq && ri < p->tol_ineq && rc < p->tol_comp;
 }
 
@@ -1030,6 +1041,7 @@ static void merit_ls(const tw_par *p, const tw_shape *sh, tw_ws *w, double *X, d
         if (an < p->ls_alpha_min) break;
         alpha = an;
     }
+    w->kkt[7] = alpha;
     for (int k = 0; k <= N; ++k) {
         for (int q = 0; q < 4; ++q) X[4 * k + q] = qfma(alpha, dxk[k][q], xk[k][q]);
         if (k < N) {
@@ -1069,6 +1081,7 @@ static void sqp_solve(const tw_par *p, const tw_shape *sh, tw_ws *w, const doubl
     o->qp_capped = 0;
     o->qp_stalled = 0;
     o->pi_written = 0;
+    memset(w->kkt, 0, sizeof w->kkt);
     if (p->nlp_mode == 1) {
         for (int k = 0; k < N; ++k)
             for (int q = 0; q < 4; ++q) w->nlpPI[4 * k + q] = PI_in ? PI_in[4 * k + q] : 0.0;
@@ -1085,7 +1098,8 @@ static void sqp_solve(const tw_par *p, const tw_shape *sh, tw_ws *w, const doubl
         for (int q = 0; q < 4; ++q) dx0[q] = x0[q] - X[q];
         int skip = was_done;
         if (p->nlp_mode == 1) {
-            const int conv = !was_done && nlp_converged(p, w->st, w->nlpPI, w->LAM);
+            const int conv = !was_done && nlp_converged(p, w->st, w->nlpPI, w->LAM, w->kkt);
+            if (!was_done) w->kkt[6] = it;
             skip = was_done || conv;
             if (conv) {
                 wdone = 1;
@@ -1344,6 +1358,7 @@ int tw_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
             if (qp_iter) qp_iter[i] = out.qp_iter;
             if (qp_capped) qp_capped[i] = out.qp_capped;
             if (qp_stalled) qp_stalled[i] = out.qp_stalled;
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)8 * i, w->kkt, sizeof w->kkt);
             if (lam) {
                 if (p.nlp_mode == 1) memcpy(lam + (size_t)i * 6 * N, w->LAM, sizeof(double) * 6 * N);
                 else memset(lam + (size_t)i * 6 * N, 0, sizeof(double) * 6 * N);
@@ -1461,6 +1476,7 @@ int tw_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
             if (qp_iter) qp_iter[i] = out.qp_iter;
             if (qp_capped) qp_capped[i] = out.qp_capped;
             if (qp_stalled) qp_stalled[i] = out.qp_stalled;
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)8 * i, w->kkt, sizeof w->kkt);
         }
         free(w);
     }
@@ -1534,6 +1550,7 @@ int tw_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
+    if (g_kkt_diag) memset(g_kkt_diag, 0, sizeof(double) * 8 * (size_t)nb);
     #pragma omp parallel
     {
         tw_ws *w = (tw_ws *)malloc(sizeof(tw_ws));
@@ -1599,6 +1616,19 @@ int tw_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
                 for (int c = 0; c < 4; ++c) x[c] = qfma(p.Ts, d.f[c], x[c]);
                 memcpy(Utraj + ((size_t)i * n_steps + t) * 2, u, sizeof u);
                 if (Straj) Straj[(size_t)i * n_steps + t] = st;
+                if (g_kkt_diag && st == 2) {
+                    /* closed loop: per lane, over its status-2 steps, how often each KKT residual
+                     * failed (stat, eq, ineq, comp), the steps, those failing stationarity alone,
+                     * and those whose stationarity residual is below 1e-3 (near misses) */
+                    double *dg = g_kkt_diag + (size_t)8 * i;
+                    const double rs = fmax(fmax(w->kkt[0], w->kkt[1]), w->kkt[2]);
+                    const int f0 = rs >= p.tol_stat, f1 = w->kkt[3] >= p.tol_eq, f2 = w->kkt[4] >= p.tol_ineq,
+                              f3 = w->kkt[5] >= p.tol_comp;
+                    dg[0] += f0; dg[1] += f1; dg[2] += f2; dg[3] += f3;
+                    dg[4] += 1.0;
+                    dg[5] += (f0 && !f1 && !f2 && !f3);
+                    dg[6] += rs < 1e-3;
+                }
             }
             memcpy(Xtraj + ((size_t)i * (n_steps + 1) + n_steps) * 4, x, sizeof x);
         }

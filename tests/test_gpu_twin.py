@@ -94,9 +94,14 @@ def test_qp_bit_identical(twin, N, S):
 
 
 def controller_pair(twin, N, B, x0, traj, sid, idx, K=50, steps=1, **kw):
-    """Cold-start controller solves (then warm-started repeats) on the GPU and on the twin."""
+    """Cold-start controller solves (then warm-started repeats) on the GPU and on the twin.  In
+    nlp_mode 1 the KKT residuals of each lane's last test (get('residuals')) are compared too."""
+    import ctypes as C
     from oracle.oracle import make_opts
     nlp = kw.pop("nlp_mode", 0)
+    diag = np.zeros((B, 8))
+    if nlp:
+        twin.L.tw_set_kkt_diag(diag.ctypes.data_as(C.c_void_p))
     s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI", **kw)
     s.set_shape_ids(sid)
     s.set_reference_trajectory(traj)
@@ -113,6 +118,12 @@ def controller_pair(twin, N, B, x0, traj, sid, idx, K=50, steps=1, **kw):
         same(s.get("u"), warm["U"], f"warm U (step {step})")
         same(s.get("pi"), warm["PI"], f"warm PI (step {step})")
         same(s.get_cost(), r["cost"], f"cost (step {step})")
+        if nlp:   # the twin records the stationarity residual by block (u, x, terminal): the device its max
+            want = np.stack([diag[:, :3].max(1), diag[:, 3], diag[:, 4], diag[:, 5]], 1)
+            same(s.get("residuals"), want, f"KKT residuals (step {step})")
+            r["kkt"] = diag.copy()
+    if nlp:
+        twin.L.tw_set_kkt_diag(None)
     s.close()
     return r
 
@@ -148,7 +159,16 @@ def test_merit_sqp_bit_identical(twin):
     from bench import SEED, make_inputs
     x0, _, _, sid, traj = make_inputs(4096, 20, SEED + 7)
     r = controller_pair(twin, 20, 4096, x0, traj, sid, 1, K=30, steps=2, nlp_mode=1)
-    assert np.mean(r["status"] == 0) > 0.15   # tol 1e-6 within 30 iterations: about a quarter of these lanes (both)
+    # Measured on the twin (= the device, bit for bit): 1 004 of 4 096 lanes meet tol 1e-6 within 30
+    # iterations at the second step (1 243 at the first), the rest end at max_iter (status 2).  Why the
+    # reference's own SQP stalls on the others -- the iterate chatters across motion-cone boundaries,
+    # where the dynamics' Jacobian jumps, and the merit line search ends at alpha_min, damping the
+    # multiplier update; exact QP duals do not change it -- is DESIGN.md section 2's residual breakdown
+    # (tests/test_merit_diagnosis.py pins it on the literal oracle).
+    assert int(np.sum(r["status"] == 0)) == 1004
+    assert set(np.unique(r["status"])) <= {0, 2}
+    st2 = r["status"] == 2
+    assert np.mean(r["kkt"][st2, :3].max(1) >= 1e-6) > 0.95   # stationarity fails on the status-2 lanes
 
 
 def test_small_batch_fused_loop_bit_identical(twin):

@@ -1,0 +1,89 @@
+"""Why the reference's own SQP configuration (acados 'sqp' + 'merit_backtracking', max_iter 30,
+tol_stat/eq/ineq/comp 1e-6: NMPC_controller.m:271-276) leaves most configs[2]-law lanes at
+max_iter (status 2) -- pinned on the CPU oracle ("Merit SQP convergence").
+
+The literal restatement (oracle/qsp_oracle.c) records, per lane, the residuals of its last KKT test
+and line-search statistics (or_set_kkt_diag), and can run with the QP's u-bound multipliers
+recovered exactly from the QP's u-stationarity (or_set_experiment(2)).  Measured:
+  * stationarity fails on almost every status-2 lane (and the equality residual on most);
+  * exact QP duals change nothing (the "dual-accuracy floor" hypothesis is refuted);
+  * the status-2 lanes' iterates chatter across motion-cone boundaries (the dynamics' Jacobian
+    jumps between sticking and sliding, PusherSliderModel.m:587-589), and their line searches end
+    at alpha_min (0.05) several times as often as on converging lanes, so the damped multiplier
+    update (alpha = 0.058) cannot close the stationarity residual within 30 iterations.
+CPU only (no GPU); the device equals the twin bit for bit (tests/test_gpu_twin.py), whose residuals
+the GPU test compares through qsp_get_residuals."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+def literal_run(B, exp=0):
+    from bench import SEED, make_inputs
+    from oracle.oracle import Oracle, lib, make_opts
+    orc = Oracle(NAMES)
+    x0, _, _, sid, traj = make_inputs(B, 20, SEED + 7)
+    op = make_opts(N=20, sqp_iters=30, nlp_mode=1, qp_iters=50)
+    diag = np.zeros((B, 18))
+    lib().or_set_kkt_diag(diag.ctypes.data_as(C.c_void_p))
+    lib().or_set_experiment(C.c_int(exp))
+    try:
+        r = orc.controller_solve(op, x0, traj, 1, orc.new_warm(B, 20), shape_id=sid)
+    finally:
+        lib().or_set_experiment(C.c_int(0))
+        lib().or_set_kkt_diag(None)
+    return r, diag
+
+
+@pytest.fixture(scope="module")
+def base():
+    return literal_run(256)
+
+
+def test_stationarity_blocks_status2(base):
+    r, d = base
+    st = r["status"]
+    assert 0.2 < np.mean(st == 0) < 0.4                     # 28 % on 512 lanes, 30 % (twin) on 4 096
+    s2 = st == 2
+    stat = d[s2, :3].max(1)
+    assert np.mean(stat >= 1e-6) > 0.95                      # measured 0.985 (384 lanes)
+    assert np.median(stat) > 1e-1                            # O(1), far above the QP dual floor (~1e-3)
+    assert np.mean(d[s2, 3] >= 1e-6) > 0.5                   # equality (defects): 0.72
+    assert np.mean(d[s2, 4] >= 1e-6) < 0.05                  # inequality: almost never
+    # converged lanes: every residual below its tolerance at the passing test
+    assert np.all(d[st == 0, :6] < 1e-6)
+
+
+def test_exact_qp_duals_do_not_help(base):
+    r0, _ = base
+    r2, _ = literal_run(256, exp=2)
+    assert abs(int(np.sum(r2["status"] == 0)) - int(np.sum(r0["status"] == 0))) <= 3
+
+
+def test_chattering_and_minimum_steps(base):
+    r, d = base
+    st = r["status"]
+    s0, s2 = st == 0, st == 2
+    # a stage's motion-cone mode changed at the last linearisation: most status-2 lanes, no
+    # converged lane (measured 0.68 / 0.00)
+    assert np.mean(d[s2, 16] > 0) > 0.5
+    assert np.mean(d[s0, 16] > 0) < 0.05
+    # line searches ending at ls_alpha_min: measured 10.8 per status-2 lane, 2.2 per converged lane
+    assert d[s2, 11].mean() > 3.0 * max(d[s0, 11].mean(), 0.5)
+
+
+def test_closed_loop_breakdown():
+    """main.m's closed loop (Hp = 10, 201 steps) on the twin: stationarity and equality dominate
+    the status-2 steps there too."""
+    from kkt_breakdown import closed_loop_breakdown
+    b = closed_loop_breakdown(48)
+    f = b["status2_fail_frac"]
+    assert f["stat"] > 0.7 and f["eq"] > 0.5 and f["ineq"] < 0.05
+    assert set(b["status"]) <= {0, 2, 4}

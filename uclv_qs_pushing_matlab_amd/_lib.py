@@ -92,6 +92,7 @@ _SIGS = {
     "qsp_get_qp_iter": [_P, _P],
     "qsp_get_qp_capped": [_P, _P],
     "qsp_get_qp_stalled": [_P, _P],
+    "qsp_get_residuals": [_P, _P],
     "qsp_get_time_tot": [_P, C.POINTER(_D)],
     "qsp_get_dims": [_P, C.POINTER(_I), C.POINTER(_I)],
     "qsp_set_yref_stage": [_P, _I, _P],

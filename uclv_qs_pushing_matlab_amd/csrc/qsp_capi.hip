@@ -60,7 +60,7 @@ struct qsp_solver {
     // per-lane controller input buffer u_buff_contr (B x D x 2, column 0 newest); closed-loop state
     int32_t D = 0;
     DevBuf ubc, ubp, cl_x, cl_xsim, cl_amp;
-    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wqp, wperm, wnit, whist;
+    DevBuf wX, wU, wx0, wlin, wnlp, wdone, wres, wqp, wperm, wnit, whist;
     DevBuf scratch[12];
     int32_t T = 0;
     bool have_traj = false;
@@ -219,6 +219,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wlin = s->wlin.as<double>();
     a.wnlp = s->wnlp.as<double>();
     a.wdone = s->wdone.as<int32_t>();
+    a.wres = s->wres.as<double>();
     a.wqp = s->wqp.as<double>();
     a.wperm = s->wperm.as<int32_t>();
     if (s->poison) a.flags |= QSP_FLAG_POISON;
@@ -424,6 +425,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
         al(s->wlin, B * (N + 1) * 24 * 8);
         al(s->wnlp, B * (N + 1) * 20 * 8);
         al(s->wqp, B * (N + 1) * 16 * 8);
+        al(s->wres, B * 4 * 8);
     }
     if (e == hipSuccess) e = hipMemsetAsync(s->shape_id.p, 0, B * 4, s->stream);
     if (e == hipSuccess) e = hipMemsetAsync(s->warm_valid.p, 0, B, s->stream);
@@ -462,7 +464,7 @@ int qsp_destroy(qsp_solver* s) {
                       &s->shapes, &s->shape_id, &s->x0, &s->yref, &s->yref_e, &s->X, &s->U, &s->PI, &s->Xo,
                       &s->Uo, &s->PIo, &s->u0, &s->status, &s->sqp_iter, &s->qp_iter, &s->qp_capped, &s->qp_stalled, &s->cost,
                       &s->warm_valid,
-                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
+                      &s->traj, &s->index_time, &s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wres, &s->wqp, &s->wperm, &s->wnit,
                       &s->whist};
     for (DevBuf* b : bufs) b->release();
     for (auto& b : s->scratch) b.release();
@@ -689,6 +691,11 @@ int qsp_get_qp_capped(qsp_solver* s, int32_t* c) {
 int qsp_get_qp_stalled(qsp_solver* s, int32_t* c) {
     if (!s || !c) return fail(QSP_ERR_ARG, "qsp_get_qp_stalled: null argument");
     return d2h(s, c, s->qp_stalled, (size_t)s->o.batch * 4);
+}
+int qsp_get_residuals(qsp_solver* s, double* res) {
+    if (!s || !res) return fail(QSP_ERR_ARG, "qsp_get_residuals: null argument");
+    if (s->o.nlp_mode != QSP_NLP_SQP_MERIT || !s->wres.p) return fail(QSP_ERR_STATE, "qsp_get_residuals: nlp_mode 1 (SQP) only");
+    return d2h(s, res, s->wres, (size_t)s->o.batch * 4 * 8);
 }
 int qsp_get_time_tot(qsp_solver* s, double* ms) {
     if (!s || !ms) return fail(QSP_ERR_ARG, "qsp_get_time_tot: null argument");

@@ -46,6 +46,8 @@ struct SolveArgs {
     double* wlin;              // 24 x B(N+1)     stage data (A, B, defect, gradient), SoA
     double* wnlp;              // 20 x B(N+1)     nlp_mode 1: PI(4), LAM(6), merit weights NU(4), ETA(6), SoA
     int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
+    double* wres;              // B x 4           nlp_mode 1: the last KKT test's residuals (stat, eq, ineq, comp;
+                               //                 nullptr: not recorded)
     double* wqp;               // 16 x B(N+1)     nlp_mode 1: QP step dx(4), du(2), multipliers pi(4), lam(6), SoA
     int32_t* wperm;            // B               wave packing order of the QP kernel (nullptr: identity)
     int32_t* wnit;             // B               IPM iterations of each instance's last four QPs (8 bits each, last lowest)

@@ -921,6 +921,8 @@ __device__ __forceinline__ void nlp_init(const SolveArgs& A, int i, bool use_pi)
         for (int q = W_LAM; q < W_COUNT; ++q) A.wnlp[q * tot + si] = 0.0;
     }
     A.wdone[i] = 0;
+    if (A.wres)
+        for (int q = 0; q < 4; ++q) A.wres[(size_t)i * 4 + q] = 0.0;
 }
 
 // With the stage-0 s bound in the QP (stage0_s_bound), s_0 = x0's s is a fixed quantity of
@@ -1053,8 +1055,11 @@ __device__ __forceinline__ double merit_stage(const SolveParams& p, int k, const
 enum QpField : int { Q_DX = 0, Q_DU = 4, Q_PI = 6, Q_LAM = 10, Q_COUNT = 16 };
 
 // KKT residuals of the NLP at the current iterate against tol_* (max norms over the
-// horizon); `nlp` points at this lane's stage in the W_* SoA (stride tot).
-__device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>& st, const double* nlp, size_t tot) {
+// horizon); `nlp` points at this lane's stage in the W_* SoA (stride tot).  res (the instance's
+// 4 doubles, or nullptr): the residuals are recorded there (acados' res_stat/eq/ineq/comp
+// statistics of the last test, qsp_get_residuals).
+__device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>& st, const double* nlp, size_t tot,
+                              double* res) {
     const int N = p.N;
     const int k = c.lig;
     const bool stg = k < N;
@@ -1104,6 +1109,12 @@ __device__ bool nlp_converged(const Ctx& c, const SolveParams& p, const Stage<1>
     re = group_max(re, c.gs);
     ri = group_max(ri, c.gs);
     rc = group_max(rc, c.gs);
+    if (res && c.real && c.lig == 0) {
+        res[0] = rs;
+        res[1] = re;
+        res[2] = ri;
+        res[3] = rc;
+    }
     return rs < p.tol_stat && re < p.tol_eq && ri < p.tol_ineq && rc < p.tol_comp;
 }
 
@@ -1240,7 +1251,8 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     if constexpr (MERIT) {
         static_assert(S == 1, "nlp_mode 1 uses one stage per lane");
         // nlp_mode 1: KKT test of the current iterate; converged instances freeze
-        const bool conv = !was_done && nlp_converged(c, p, st, A.wnlp + (size_t)iv * (N + 1) + c.lig, tot);
+        const bool conv = !was_done && nlp_converged(c, p, st, A.wnlp + (size_t)iv * (N + 1) + c.lig, tot,
+                                                     A.wres ? A.wres + (size_t)iv * 4 : nullptr);
         skip = was_done || conv || !c.real;
         if (conv && c.real && c.lig == 0) {
             A.wdone[iv] = 1;

@@ -211,6 +211,10 @@ class OcpSolver:
                   "qp_stalled": self._L.qsp_get_qp_stalled}[field]
             check(fn(self._h, ptr(out)), f"get('{field}')")
             return out
+        if field == "residuals":   # acados res_stat/eq/ineq/comp of the last KKT test (nlp_mode 1)
+            out = np.zeros((B, 4))
+            check(self._L.qsp_get_residuals(self._h, ptr(out)), "get('residuals')")
+            return out
         if field == "time_tot":
             ms = C.c_double()
             check(self._L.qsp_get_time_tot(self._h, C.byref(ms)), "get('time_tot')")
