@@ -159,20 +159,25 @@ def flops_per_solve(N, K, qp_iter_total):
     return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
 
 
-def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20):
+def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20, idx=1):
     """The CPU restatement (port) timed on a bounded sample of the same workload (cold-start
     controller solves): the kernel-order twin (twin=True: the library's formulation on the CPU,
-    OpenMP over lanes) or the literal oracle."""
+    OpenMP over lanes) or the literal oracle.  idx: index_time (scalar, or per lane)."""
     from oracle.oracle import Oracle, make_opts
     orc = Oracle(SHAPES, twin=twin)
     op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=qp_iters)
+    idx_all = np.broadcast_to(np.asarray(idx, np.int32), (len(x0),))
 
-    def run(sl, xx=None, K_run=K, **kw):
+    def run(sl, xx=None, K_run=K, nthreads=None, precision=None, **kw):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
         o = op if (K_run == K and not kw) else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode,
                                                          **dict(dict(qp_iters=qp_iters), **kw))
-        return orc.controller_solve(o, xx, traj, 1, warm, shape_id=shape_id[sl], nthreads=threads)
+        nt = threads if nthreads is None else nthreads
+        if precision is not None:   # the literal restatement in long double / __float128 (oracle OR_EXT)
+            return orc.controller_solve_ext(o, xx, traj, idx_all[sl], warm, shape_id=shape_id[sl], nthreads=nt,
+                                            precision=precision)
+        return orc.controller_solve(o, xx, traj, idx_all[sl], warm, shape_id=shape_id[sl], nthreads=nt)
 
     probe = min(len(x0), max(2 * threads, 16))
     t0 = time.perf_counter()
@@ -186,7 +191,72 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=T
     return n, dt, r, run
 
 
-def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_iters=20):
+def thread_scaling(run, rate_all, threads, aff, seconds=1.5):
+    """The twin's solves/s on 1 and 4 threads (short samples) beside the job's `threads`: lanes are
+    independent, so the rate scales with the cores given; `full_host_estimate` extrapolates the
+    per-thread rate at `threads` to every CPU of the affinity mask (the GPU box allots this job
+    `threads` of them: a run on all of them is not this job's to make)."""
+    out = {"threads": [], "solves_per_s": []}
+    for t in (1, 4):
+        if t >= threads:
+            continue
+        t0 = time.perf_counter()
+        run(slice(0, 2 * t), nthreads=t)
+        per = (time.perf_counter() - t0) / (2 * t)
+        n = max(t, int(seconds / max(per, 1e-7) * t) // t * t)
+        t0 = time.perf_counter()
+        run(slice(0, n), nthreads=t)
+        out["threads"].append(t)
+        out["solves_per_s"].append(n / (time.perf_counter() - t0))
+    out["threads"].append(threads)
+    out["solves_per_s"].append(rate_all)
+    out["efficiency_vs_1_thread"] = (rate_all / threads) / out["solves_per_s"][0] if out["threads"][0] == 1 else None
+    out["full_host_estimate"] = {"cpus": aff, "solves_per_s": rate_all / threads * aff,
+                                 "note": f"per-thread rate at {threads} threads x {aff} CPUs (linear scaling: an "
+                                         "upper bound for the CPU)"}
+    return out
+
+
+def extended_adjudication(u_gpu, u_lit, run, lanes_sets, max_lanes=64, control=None):
+    """Where the GPU and the double literal restatement disagree by > 1e-6: the literal formulas in
+    __float128 (and long double), the exact-arithmetic answer as far as the SQP's amplification
+    allows (long double and quad agreeing to 1e-6 marks that), and which implementation it sides with
+    (tests/tools/ext_adjudicate.py).  lanes_sets: (name, lane indices) in
+    priority order, capped at max_lanes in total; control: lanes where both agree."""
+    picked, names = [], []
+    for name, ls in lanes_sets:
+        for l in ls:
+            if len(picked) < max_lanes and l not in picked:
+                picked.append(int(l))
+                names.append(name)
+    lanes = np.array(picked + [int(c) for c in (control if control is not None else [])], dtype=np.int64)
+    if len(lanes) == 0:
+        return {"lanes": 0}
+    t0 = time.perf_counter()
+    uq = run(lanes, precision="quad")["u0"]
+    ul = run(lanes, precision="long")["u0"]
+    dt = np.abs(u_gpu[lanes] - uq).max(1)
+    dl = np.abs(u_lit[lanes] - uq).max(1)
+    ext_ok = np.abs(ul - uq).max(1) <= 1e-6
+    side = np.where((dt <= 1e-6) & (dl > 1e-6), "gpu", np.where((dl <= 1e-6) & (dt > 1e-6), "literal",
+                    np.where((dt <= 1e-6) & (dl <= 1e-6), "both", "neither")))
+    out = {"reference": "oracle/qsp_oracle.c in __float128 (libquadmath) and long double, the same formulas",
+           "seconds": time.perf_counter() - t0}
+    for name in dict.fromkeys(names):
+        m = np.array([nm == name for nm in names] + [False] * (len(lanes) - len(names)))
+        out[name] = {"lanes": int(m.sum()), "ext_stable": int(np.sum(m & ext_ok)),
+                     **{f"sides_with_{k}": int(np.sum(m & (side == k))) for k in ("gpu", "literal", "both", "neither")}}
+        if name == "stable_in_both":
+            out[name]["per_lane"] = [{"lane": int(lanes[j]), "side": str(side[j]), "gpu_err": float(dt[j]),
+                                      "literal_err": float(dl[j])} for j in np.flatnonzero(m)]
+    if control is not None and len(control):
+        m = np.arange(len(lanes)) >= len(names)
+        out["control_agreeing_lanes"] = {"lanes": int(m.sum()), "gpu_within_1e-6_of_quad": int(np.sum(m & (dt <= 1e-6))),
+                                         "literal_within_1e-6_of_quad": int(np.sum(m & (dl <= 1e-6)))}
+    return out
+
+
+def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_iters=20, extended=True, ext_lanes=48):
     """GPU u0 vs oracle u0 on the whole CPU sample (n lanes), with the oracle's own sensitivity
     as the yardstick: a lane is chaotic when the oracle's u0 moves by > 1e-9 under
     three 1e-13 relative perturbations of x0 or when mu_stop moves 1e-10 -> 1.5e-10; parity is
@@ -224,6 +294,20 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_ite
         out["gpu_chaotic_frac"] = float(gc.mean())
         out["chaotic_overlap_jaccard"] = float((gc & rc).sum() / max(int((gc | rc).sum()), 1))
         out["frac_err_gt_1e-6_stable_in_both"] = float(np.mean((d > 1e-6) & ~gc & ~rc))
+    if extended:
+        # the disagreements adjudicated in extended precision: first the lanes stable in both
+        # implementations, then those the literal's probes call stable, then the others
+        dis = d > 1e-6
+        lit_stable = dis & (self_dev <= 1e-6) & (mod_dev <= 1e-6)
+        both = lit_stable & (gpu_dev[:n] <= 1e-6) if gpu_dev is not None else np.zeros(n, bool)
+        rng = np.random.default_rng(3)
+        rest = np.flatnonzero(dis & ~lit_stable)
+        agree = np.flatnonzero(~dis)
+        out["extended_precision"] = extended_adjudication(
+            u0_gpu[:n], u0_ref, run,
+            [("stable_in_both", np.flatnonzero(both)), ("literal_stable", np.flatnonzero(lit_stable & ~both)),
+             ("other_disagreeing", rng.permutation(rest))],
+            max_lanes=ext_lanes, control=np.sort(rng.choice(agree, min(ext_lanes // 2, len(agree)), replace=False)))
     if nlp == "SQP_RTI":
         # the same statistics with round 1's QP stop rule (mu and bound residual < 1e-10, cap 20,
         # no stage-0 s bound), on the first lanes: the chaotic fraction does not depend on it
@@ -708,6 +792,11 @@ def main():
                               "layout": {"stages_per_lane": S4, "lanes_per_instance": L4},
                               "note": "host-boundary controller solves (x0 in, u0 out), 3 repeats"}
         u4_gpu = s4.get_u0()
+        # the GPU's own response to the literal parity leg's 1e-13 x0 probes (untimed)
+        gpu_dev4 = np.zeros(len(x4))
+        for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+            s4.controller_reset()
+            gpu_dev4 = np.maximum(gpu_dev4, np.abs(s4.controller_solve(x4 * (1 + sgn * f * 1e-13), idx4b) - u4_gpu).max(1))
         s4.close()
 
     if rank == 0 and world == 1 and not args.no_closed_loop and not cfg4 and args.nlp == "SQP_RTI":
@@ -729,6 +818,7 @@ def main():
                                   "cpu_model": hc["model"],
                                   "sample": f"{n} lanes of the same workload (oracle/qsp_twin.c: the library's "
                                             f"formulation on the CPU, OpenMP over {threads} threads, {dt:.1f} s)"}
+        result["cpu_baseline"]["thread_scaling"] = thread_scaling(run_t, n / dt, threads, hc["affinity_cpus"])
         # bit-exact parity: every lane of the batch against the twin (the CPU sample above included)
         from oracle.oracle import Oracle, make_opts
         tw = Oracle(SHAPES, twin=True)
@@ -773,6 +863,15 @@ def main():
             result["configs4"].update({"lanes": int(len(x4)), "cpu_seconds": time.perf_counter() - t4c,
                                        "bit_identical_u0_lanes": int(np.sum(np.all(u4_gpu == r4["u0"], axis=1))),
                                        "status_nonzero_lanes": int(np.count_nonzero(r4["status"]))})
+            # and the literal restatement on the first 1 024 lanes, with its probes and the extended-
+            # precision adjudication of the disagreements (as parity_literal above)
+            n4 = min(1024, len(x4))
+            _, _, r4l, run4 = cpu_baseline(x4[:n4], traj4, sid4[:n4], 50, K, 0.0, threads, 0, twin=False,
+                                           qp_iters=args.qp_iters, idx=idx4b[:n4])
+            r4l = run4(slice(0, n4))
+            pl4 = parity_leg(u4_gpu[:n4], x4[:n4], traj4, sid4[:n4], 50, K, n4, r4l, run4, "SQP_RTI_N50",
+                             gpu_dev4[:n4], qp_iters=args.qp_iters, ext_lanes=16)
+            result["configs4"]["parity_literal"] = pl4
     if rank == 0:
         if nbad:
             print(f"bench: WARNING {nbad} of {total} lanes returned a non-zero status", file=sys.stderr)

@@ -218,8 +218,8 @@ int qsp_get_reference_trajectories(qsp_solver* s, double* traj);
  * shifted after every call; u0 is available through qsp_get_u0. */
 int qsp_controller_solve(qsp_solver* s, const double* x0, const int32_t* index_time);
 int qsp_controller_reset(qsp_solver* s);                                                 /* clear_variables */
-/* Closed-loop simulation on the device (helper.m:195-322, closed_loop_matlab): cold start,
- * then for t = 0..n_steps-1: x += noise[t] (sim_noise, optional), u = solve(x, index0 + t),
+/* Closed-loop simulation on the device (helper.m:195-322, closed_loop_matlab): cold start of the
+ * solver's warm start (X, U, PI), then for t = 0..n_steps-1: x += noise[t] (sim_noise, optional), u = solve(x, index0 + t),
  * x += Ts * f(x, u) (evalModelVariableShape + Euler, :292-307).  x0: B x 4; index0: B (1-based);
  * noise: n_steps x B x 4 or NULL; X_traj: B x (n_steps+1) x 4; U_traj: B x n_steps x 2;
  * status_traj: B x n_steps (found_sol = status == 0) or NULL. */
@@ -237,13 +237,18 @@ typedef struct {
 /* Per step i: disturbance (i == t_dist), noise, the controller's delay prediction (delay_buffer_sim
  * with the handle's delay compensation), u = solve(x_sim, index0 + i - 1 + delay_buff_comp), the
  * controller buffer push, the (delayed) plant step.  X_traj: the plant states after disturbance and
- * noise (B x (n+1) x 4); X_sim (optional): the states handed to the solver (B x n x 4). */
+ * noise (B x (n+1) x 4); X_sim (optional): the states handed to the solver (B x n x 4).
+ * State carried between calls: the controller's input buffer u_buff_contr is the controller
+ * object's (NMPC_controller.m:109), as in helper.m, where it persists across closed_loop_matlab
+ * calls: it is NOT reset here (a second closed loop on the same handle starts from the buffer the
+ * first one left); only qsp_set_delay_comp zeroes it.  The plant's buffer u_buff_plant is local
+ * to one call (helper.m:211-212) and starts at zero.  Both closed-loop entry points behave so. */
 int qsp_closed_loop_ex(qsp_solver* s, const qsp_closed_loop_opts* opts, const double* x0, const int32_t* index0,
                        int32_t n_steps, const double* noise, double* X_traj, double* X_sim, double* U_traj,
                        int32_t* status_traj);
 /* set_delay_comp (NMPC_controller.m:106-110): delay_buff_comp = ceil(delay / Ts) columns; the
  * reference table is read as set_reference_trajectory prepends it (:425-431) and the per-lane input
- * buffer u_buff_contr is zeroed.  get: the column count. */
+ * buffer u_buff_contr is zeroed (the only call that zeroes it).  get: the column count. */
 int qsp_set_delay_comp(qsp_solver* s, double delay);
 int qsp_get_delay_comp(qsp_solver* s, int32_t* cols);
 /* delay_buffer_sim (NMPC_controller.m:112-120): x (B x 4) advanced by delay_buff_comp Euler steps with

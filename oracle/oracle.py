@@ -225,6 +225,31 @@ class Oracle:
             self.L.or_controller_solve(*args, _p(stalled))
         return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped, qp_stalled=stalled)
 
+    def controller_solve_ext(self, opts, x0, traj, index_time, warm, shape_id=None, nthreads=0, delay_cols=0,
+                             precision="quad"):
+        """controller_solve of the LITERAL restatement evaluated in extended precision (qsp_oracle.c
+        built with OR_EXT: "long" = long double, "quad" = __float128); double in/out."""
+        if self.twin:
+            raise ValueError("extended precision: literal restatement only")
+        N = opts.N
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 4)
+        nb = len(x0)
+        sid = self._ids(shape_id, nb)
+        traj = np.ascontiguousarray(traj, np.float64).reshape(-1, 6)
+        idx = np.ascontiguousarray(np.broadcast_to(np.asarray(index_time, np.int32), (nb,)), np.int32)
+        u0 = np.zeros((nb, 2))
+        status = np.zeros(nb, np.int32)
+        iters = np.zeros(nb, np.int32)
+        qp_iter = np.zeros(nb, np.int32)
+        cost = np.zeros(nb)
+        fn = {"long": self.L.orx_controller_solve_l, "quad": self.L.orx_controller_solve_q}[precision]
+        r = fn(*self._shape_args(), C.c_int32(len(self._n)), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
+               C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]), _p(warm["valid"]), _p(u0),
+               _p(status), _p(iters), _p(qp_iter), _p(cost), C.c_int(nthreads), C.c_int32(int(delay_cols)))
+        if r != 0:
+            raise ValueError("orx_controller_solve: bad arguments")
+        return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
+
     def closed_loop(self, opts, x0, traj, n_steps, index0=1, shape_id=None, noise=None, delay_cols=0,
                     plant_delay_cols=0, dist_step=0, dist_amp=None, xwidth=None, nthreads=0, ubc0=None):
         """helper.m:195-322 closed loop (see or_closed_loop).  Returns X (nb, n+1, 4), Xsim (nb, n, 4),

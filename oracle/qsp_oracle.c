@@ -37,6 +37,35 @@
 #include <omp.h>
 #endif
 
+/* The scalar type of the restatement.  Default: real = double (the or_* API).  Built a second
+ * time with OR_EXT = 1 (long double, 64-bit significand) or OR_EXT = 2 (__float128, 113-bit,
+ * libquadmath) it is the extended-precision oracle: the same formulas evaluated 2^11 / 2^60 times
+ * more finely, exported as orx_controller_solve (double in/out, converted at the boundary) to
+ * adjudicate the lanes where the kernel-order twin and the double restatement disagree
+ * (tests/test_extended_oracle.py). */
+#if defined(OR_EXT) && OR_EXT == 2
+#include <quadmath.h>
+typedef __float128 real;
+#undef isfinite
+#define isfinite(x) finiteq(x)
+#define sin(x) sinq(x)
+#define cos(x) cosq(x)
+#define sqrt(x) sqrtq(x)
+#define fabs(x) fabsq(x)
+#define fmod(x, y) fmodq(x, y)
+#define floor(x) floorq(x)
+#elif defined(OR_EXT) && OR_EXT == 1
+#include <tgmath.h>
+typedef long double real;
+#else
+typedef double real;
+#endif
+#ifdef OR_EXT
+#define OR_EXPORT static   /* the extended build exports orx_controller_solve only */
+#else
+#define OR_EXPORT
+#endif
+
 #define NX 4
 #define NU 2
 #define NDIR 6 /* AD directions: x, y, theta, s, u_n, u_t */
@@ -46,24 +75,24 @@
 /* ------------------------------------------------------------------ shapes */
 typedef struct {
     int n;              /* number of control points (after closing the loop) */
-    const double *P;    /* n x 2, row-major */
-    const double *S;    /* n + 4 knots */
-    double b;           /* contour length (bspline_shape.m:37) */
-    double c;           /* c_ellipse = tau_max / (mu_sg m g)  (PusherSliderModel.m:53,55) */
-    double mu;          /* mu_sp */
+    const real *P;    /* n x 2, row-major */
+    const real *S;    /* n + 4 knots */
+    real b;           /* contour length (bspline_shape.m:37) */
+    real c;           /* c_ellipse = tau_max / (mu_sg m g)  (PusherSliderModel.m:53,55) */
+    real mu;          /* mu_sp */
 } or_shape;
 
 #include "or_opts.h"
 
 /* ================================================================ dual numbers */
-typedef struct { double v, d[NDIR]; } dual;
+typedef struct { real v, d[NDIR]; } dual;
 
-static inline dual dc(double v) { dual r; r.v = v; for (int i = 0; i < NDIR; ++i) r.d[i] = 0.0; return r; }
+static inline dual dc(real v) { dual r; r.v = v; for (int i = 0; i < NDIR; ++i) r.d[i] = 0.0; return r; }
 static inline dual dadd(dual a, dual b) { dual r; r.v = a.v + b.v; for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
 static inline dual dsub(dual a, dual b) { dual r; r.v = a.v - b.v; for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
 static inline dual dneg(dual a) { dual r; r.v = -a.v; for (int i = 0; i < NDIR; ++i) r.d[i] = -a.d[i]; return r; }
 static inline dual dmul(dual a, dual b) { dual r; r.v = a.v * b.v; for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
-static inline dual dscale(dual a, double s) { dual r; r.v = a.v * s; for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] * s; return r; }
+static inline dual dscale(dual a, real s) { dual r; r.v = a.v * s; for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] * s; return r; }
 static inline dual ddiv(dual a, dual b) {
     dual r; r.v = a.v / b.v;
     for (int i = 0; i < NDIR; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) / b.v;
@@ -74,8 +103,8 @@ static inline dual dsqrt(dual a) {
     for (int i = 0; i < NDIR; ++i) r.d[i] = a.d[i] / (2.0 * r.v);
     return r;
 }
-static inline dual dsin(dual a) { dual r; r.v = sin(a.v); double c = cos(a.v); for (int i = 0; i < NDIR; ++i) r.d[i] = c * a.d[i]; return r; }
-static inline dual dcos(dual a) { dual r; r.v = cos(a.v); double s = -sin(a.v); for (int i = 0; i < NDIR; ++i) r.d[i] = s * a.d[i]; return r; }
+static inline dual dsin(dual a) { dual r; r.v = sin(a.v); real c = cos(a.v); for (int i = 0; i < NDIR; ++i) r.d[i] = c * a.d[i]; return r; }
+static inline dual dcos(dual a) { dual r; r.v = cos(a.v); real s = -sin(a.v); for (int i = 0; i < NDIR; ++i) r.d[i] = s * a.d[i]; return r; }
 /* indicator: derivative is zero (CasADi comparison operators) */
 static inline dual dind(int cond) { return dc(cond ? 1.0 : 0.0); }
 
@@ -83,27 +112,27 @@ static inline dual dind(int cond) { return dc(cond ? 1.0 : 0.0); }
 /* Cox–de Boor recursion with value and d/ds, 1-based knot index i, as
  * bspline_shape.m:40-72: zero-support guard :46, half-open indicator :52,
  * zero-denominator guards :59-68. */
-static void basis(const double *S1 /* 1-based */, double s, int i, int ord, double *N, double *dN)
+static void basis(const real *S1 /* 1-based */, real s, int i, int ord, real *N, real *dN)
 {
     if (S1[i + ord + 1] == S1[i]) { *N = 0.0; *dN = 0.0; return; }
     if (ord == 0) { *N = ((s < S1[i + 1]) && (s >= S1[i])) ? 1.0 : 0.0; *dN = 0.0; return; }
-    double N1, dN1, N2, dN2;
+    real N1, dN1, N2, dN2;
     basis(S1, s, i, ord - 1, &N1, &dN1);
     basis(S1, s, i + 1, ord - 1, &N2, &dN2);
-    double m1 = 0.0, dm1 = 0.0, m2 = 0.0, dm2 = 0.0;
-    if (S1[i + ord] != S1[i]) { double den = S1[i + ord] - S1[i]; m1 = (s - S1[i]) / den; dm1 = 1.0 / den; }
-    if (S1[i + ord + 1] != S1[i + 1]) { double den = S1[i + ord + 1] - S1[i + 1]; m2 = (S1[i + ord + 1] - s) / den; dm2 = -1.0 / den; }
+    real m1 = 0.0, dm1 = 0.0, m2 = 0.0, dm2 = 0.0;
+    if (S1[i + ord] != S1[i]) { real den = S1[i + ord] - S1[i]; m1 = (s - S1[i]) / den; dm1 = 1.0 / den; }
+    if (S1[i + ord + 1] != S1[i + 1]) { real den = S1[i + ord + 1] - S1[i + 1]; m2 = (S1[i + ord + 1] - s) / den; dm2 = -1.0 / den; }
     *N = m1 * N1 + m2 * N2;
     *dN = (dm1 * N1 + m1 * dN1) + (dm2 * N2 + m2 * dN2);
 }
 
 /* FC(s) = sum_i N_{i,3}(s) P_i  (getSymbolicSpline, bspline_shape.m:74-83) */
-static void spline_C(const or_shape *sh, double s, double C[2], double dC[2])
+static void spline_C(const or_shape *sh, real s, real C[2], real dC[2])
 {
-    const double *S1 = sh->S - 1;
+    const real *S1 = sh->S - 1;
     C[0] = C[1] = dC[0] = dC[1] = 0.0;
     for (int i = 1; i <= sh->n; ++i) {
-        double N, dN;
+        real N, dN;
         basis(S1, s, i, 3, &N, &dN);
         C[0] += N * sh->P[2 * (i - 1) + 0];
         C[1] += N * sh->P[2 * (i - 1) + 1];
@@ -114,18 +143,18 @@ static void spline_C(const or_shape *sh, double s, double C[2], double dC[2])
 
 /* FC_dot(s) = sum_{i>=2} cj_1(i) N_{i,2}(s), cj_1 = p (P_i - P_{i-1})/(S_{i+p} - S_i)
  * (getSymboliSplineDot, bspline_shape.m:85-104) */
-static void spline_Cdot(const or_shape *sh, double s, double D[2], double dD[2])
+static void spline_Cdot(const or_shape *sh, real s, real D[2], real dD[2])
 {
-    const double *S1 = sh->S - 1;
+    const real *S1 = sh->S - 1;
     D[0] = D[1] = dD[0] = dD[1] = 0.0;
     for (int i = 2; i <= sh->n; ++i) {
-        double cx = 0.0, cy = 0.0;
+        real cx = 0.0, cy = 0.0;
         if (S1[i + 3] != S1[i]) {
-            double den = S1[i + 3] - S1[i];
+            real den = S1[i + 3] - S1[i];
             cx = 3.0 * ((sh->P[2 * (i - 1) + 0] - sh->P[2 * (i - 2) + 0]) / den);
             cy = 3.0 * ((sh->P[2 * (i - 1) + 1] - sh->P[2 * (i - 2) + 1]) / den);
         }
-        double N, dN;
+        real N, dN;
         basis(S1, s, i, 2, &N, &dN);
         D[0] += cx * N; D[1] += cy * N;
         dD[0] += cx * dN; dD[1] += cy * dN;
@@ -133,13 +162,13 @@ static void spline_Cdot(const or_shape *sh, double s, double D[2], double dD[2])
 }
 
 /* s_mod inside the OCP model: fmod(s,b) + (s<0) b  (PusherSliderModel.m:526) */
-static double smod_model(double s, double b) { return fmod(s, b) + ((s < 0.0) ? b : 0.0); }
+static real smod_model(real s, real b) { return fmod(s, b) + ((s < 0.0) ? b : 0.0); }
 
 /* MATLAB floor-mod  mod(a,b) = a - floor(a/b) b   (NMPC_controller.m:320,332) */
-static double mat_mod(double a, double b)
+static real mat_mod(real a, real b)
 {
     if (b == 0.0) return a;
-    double r = a - floor(a / b) * b;
+    real r = a - floor(a / b) * b;
     if (r == b) r = 0.0;
     return r;
 }
@@ -149,7 +178,7 @@ static double mat_mod(double a, double b)
 /* motion-cone modes of the dynamics evaluations since the last reset, base 4 (diagnostics only) */
 static __thread int g_mode_code = 0;
 
-static void dynamics(const or_shape *sh, const double x[4], const double u[2], double f[4], double *J)
+static void dynamics(const or_shape *sh, const real x[4], const real u[2], real f[4], real *J)
 {
     dual X[4], U[2];
     for (int i = 0; i < 4; ++i) { X[i] = dc(x[i]); X[i].d[i] = 1.0; }
@@ -159,7 +188,7 @@ static void dynamics(const or_shape *sh, const double x[4], const double u[2], d
     dual sig = X[3];
     sig.v = smod_model(x[3], sh->b);
 
-    double C[2], dC[2], D[2], dD[2];
+    real C[2], dC[2], D[2], dD[2];
     spline_C(sh, sig.v, C, dC);
     spline_Cdot(sh, sig.v, D, dD);
     dual Px = dc(C[0]), Py = dc(C[1]), Dx = dc(D[0]), Dy = dc(D[1]);
@@ -176,8 +205,8 @@ static void dynamics(const or_shape *sh, const double x[4], const double u[2], d
     dual py = dadd(dmul(tx, Px), dmul(ty, Py));
 
     dual sn = dsin(X[2]), cs = dcos(X[2]);
-    double c = sh->c, mu = sh->mu;
-    double c2 = c * c;
+    real c = sh->c, mu = sh->mu;
+    real c2 = c * c;
     dual px2 = dmul(px, px), py2 = dmul(py, py), pxpy = dmul(px, py);
     dual fac = ddiv(dc(1.0), dadd(dadd(dc(c2), px2), py2));                              /* :544 */
     dual gl = ddiv(dadd(dsub(dc(mu * c2), pxpy), dscale(px2, mu)),
@@ -229,29 +258,29 @@ static void dynamics(const or_shape *sh, const double x[4], const double u[2], d
 }
 
 /* tangent-angle rate kappa(s) = d/ds atan2(C'_y, C'_x) (bspline_shape.m:137-152) */
-static double angle_rate(const or_shape *sh, double s)
+static real angle_rate(const or_shape *sh, real s)
 {
-    double D[2], dD[2];
+    real D[2], dD[2];
     spline_Cdot(sh, s, D, dD);
     return (D[0] * dD[1] - D[1] * dD[0]) / (D[0] * D[0] + D[1] * D[1]);
 }
 
 /* v_bound(s)  (NMPC_controller.m:319-327) */
-static double v_bound(const or_shape *sh, const or_opts *o, double s)
+static real v_bound(const or_shape *sh, const or_opts *o, real s)
 {
-    double sm = mat_mod(s, sh->b);
-    double ta = fabs(angle_rate(sh, sm));
-    double v = o->v_alpha / (fabs(ta - o->t_angle0) + 0.0001) + o->d_v;
+    real sm = mat_mod(s, sh->b);
+    real ta = fabs(angle_rate(sh, sm));
+    real v = o->v_alpha / (fabs(ta - o->t_angle0) + 0.0001) + o->d_v;
     return v < o->u_t_ub ? v : o->u_t_ub;
 }
 
 /* ================================================================ RK4 + VDE */
-static const double RK_A[4] = {0.0, 0.5, 0.5, 1.0};
-static const double RK_B[4] = {1.0 / 6.0, 1.0 / 3.0, 1.0 / 3.0, 1.0 / 6.0};
+static const real RK_A[4] = {0.0, 0.5, 0.5, 1.0};
+static const real RK_B[4] = {(real)1 / 6, (real)1 / 3, (real)1 / 3, (real)1 / 6};
 
 /* The model probe (or_opts.model_probe): set by the solve entry points before their parallel
  * region, read-only inside it. */
-static double g_probe_eps = 0.0;
+static real g_probe_eps = 0.0;
 static uint64_t g_probe_seed = 0;
 
 static inline uint64_t mix64(uint64_t z)
@@ -262,16 +291,16 @@ static inline uint64_t mix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
-static void probe_outputs(const double x[4], const double u[2], double xn[4], double A[16], double B[8])
+static void probe_outputs(const real x[4], const real u[2], real xn[4], real A[16], real B[8])
 {
     uint64_t h = mix64(g_probe_seed);
     for (int i = 0; i < 4; ++i) { uint64_t b; memcpy(&b, &x[i], 8); h = mix64(h ^ b); }
     for (int i = 0; i < 2; ++i) { uint64_t b; memcpy(&b, &u[i], 8); h = mix64(h ^ b); }
-    double *out[3] = {xn, A, B};
+    real *out[3] = {xn, A, B};
     const int len[3] = {4, 16, 8};
     int e = 0;
     for (int a = 0; a < 3; ++a) {
-        double scale = 0.0;   /* the array's largest entry: differences between formulations are
+        real scale = 0.0;   /* the array's largest entry: differences between formulations are
                                  absolute at that scale, not relative to each (possibly tiny) entry */
         for (int i = 0; i < len[a]; ++i) scale = fmax(scale, fabs(out[a][i]));
         for (int i = 0; i < len[a]; ++i, ++e) {
@@ -282,39 +311,39 @@ static void probe_outputs(const double x[4], const double u[2], double xn[4], do
 }
 
 /* x+ = phi(x,u) and A = dphi/dx (4x4), B = dphi/du (4x2), row-major */
-static void rk4_sens(const or_shape *sh, double h, const double x[4], const double u[2],
-                     double xn[4], double A[16], double B[8])
+static void rk4_sens(const or_shape *sh, real h, const real x[4], const real u[2],
+                     real xn[4], real A[16], real B[8])
 {
-    double Sx[4][6];   /* sensitivity of current stage state wrt (x0,u) */
-    double K[4][4], SK[4][4][6];
+    real Sx[4][6];   /* sensitivity of current stage state wrt (x0,u) */
+    real K[4][4], SK[4][4][6];
     for (int st = 0; st < 4; ++st) {
-        double xs[4];
+        real xs[4];
         for (int i = 0; i < 4; ++i) {
             xs[i] = x[i];
             for (int j = 0; j < 6; ++j) Sx[i][j] = (i == j) ? 1.0 : 0.0;
         }
         if (st > 0) {
-            double a = h * RK_A[st];
+            real a = h * RK_A[st];
             for (int i = 0; i < 4; ++i) {
                 xs[i] += a * K[st - 1][i];
                 for (int j = 0; j < 6; ++j) Sx[i][j] += a * SK[st - 1][i][j];
             }
         }
-        double J[24];
+        real J[24];
         dynamics(sh, xs, u, K[st], J);
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 6; ++j) {
-                double acc = (j >= 4) ? J[i * 6 + j] : 0.0;
+                real acc = (j >= 4) ? J[i * 6 + j] : 0.0;
                 for (int m = 0; m < 4; ++m) acc += J[i * 6 + m] * Sx[m][j];
                 SK[st][i][j] = acc;
             }
     }
     for (int i = 0; i < 4; ++i) {
-        double acc = x[i];
-        double S[6];
+        real acc = x[i];
+        real S[6];
         for (int j = 0; j < 6; ++j) S[j] = (i == j) ? 1.0 : 0.0;
         for (int st = 0; st < 4; ++st) {
-            double w = h * RK_B[st];
+            real w = h * RK_B[st];
             acc += w * K[st][i];
             for (int j = 0; j < 6; ++j) S[j] += w * SK[st][i][j];
         }
@@ -329,20 +358,20 @@ static void rk4_sens(const or_shape *sh, double h, const double x[4], const doub
 /* Bounded components per stage: 0 = s (x[3]), 1 = u_n (u[0]), 2 = u_t (u[1]) */
 typedef struct {
     int N;
-    const double *A, *B, *b;     /* N x 16, N x 8, N x 4 */
-    const double *H;             /* N x 6 stage diag Hessian, + 4 terminal (at H + 6N) */
-    const double *g;             /* N x 6 stage gradient, + 4 terminal */
-    const double *lo, *hi;       /* N x 3 bounds in step space */
+    const real *A, *B, *b;     /* N x 16, N x 8, N x 4 */
+    const real *H;             /* N x 6 stage diag Hessian, + 4 terminal (at H + 6N) */
+    const real *g;             /* N x 6 stage gradient, + 4 terminal */
+    const real *lo, *hi;       /* N x 3 bounds in step space */
     const uint8_t *act;          /* N x 3 active flags */
-    double dx0[4];
+    real dx0[4];
 } or_qp;
 
 typedef struct {
-    double *dx;   /* (N+1) x 4 */
-    double *du;   /* N x 2 */
-    double *pi;   /* N x 4 */
-    double *lam;  /* N x 3 x 2 (lo, hi) */
-    double *t;    /* N x 3 x 2 */
+    real *dx;   /* (N+1) x 4 */
+    real *du;   /* N x 2 */
+    real *pi;   /* N x 4 */
+    real *lam;  /* N x 3 x 2 (lo, hi) */
+    real *t;    /* N x 3 x 2 */
 } or_qp_sol;
 
 /* Experiments on the merit SQP (tests/tools/kkt_breakdown.py; 0 = the reference's algorithm):
@@ -350,74 +379,74 @@ typedef struct {
  *   2 the QP's u-bound multipliers recovered from its u-stationarity (exact QP duals),
  *   4 no minimum step: backtrack down to 1e-12 instead of accepting the step at ls_alpha_min. */
 static int g_exp = 0;
-void or_set_experiment(int flags) { g_exp = flags; }
+OR_EXPORT void or_set_experiment(int flags) { g_exp = flags; }
 
-static void inv2(const double R[4], double Ri[4])
+static void inv2(const real R[4], real Ri[4])
 {
-    double det = R[0] * R[3] - R[1] * R[2];
-    double id = 1.0 / det;
+    real det = R[0] * R[3] - R[1] * R[2];
+    real id = 1.0 / det;
     Ri[0] = R[3] * id; Ri[1] = -R[1] * id; Ri[2] = -R[2] * id; Ri[3] = R[0] * id;
 }
 
 /* Riccati factor + solve of the barrier-modified LQ problem.
  * Hd: N x 6 diag Hessian incl. barrier; gd: N x 6 gradient; terminal from qp.
  * If factor != 0 computes and stores K, Ri, Pb; otherwise reuses them. */
-typedef struct { double K[OR_MAX_N][8], kk[OR_MAX_N][2], Ri[OR_MAX_N][4], Pb[OR_MAX_N][4]; } or_fact;
+typedef struct { real K[OR_MAX_N][8], kk[OR_MAX_N][2], Ri[OR_MAX_N][4], Pb[OR_MAX_N][4]; } or_fact;
 
-static void riccati(const or_qp *qp, const double *Hd, const double *gd, or_fact *F, int factor,
-                    double *dx /* (N+1)x4 */, double *du /* N x 2 */)
+static void riccati(const or_qp *qp, const real *Hd, const real *gd, or_fact *F, int factor,
+                    real *dx /* (N+1)x4 */, real *du /* N x 2 */)
 {
     int N = qp->N;
-    double P[16] = {0}, p[4];
+    real P[16] = {0}, p[4];
     for (int i = 0; i < 4; ++i) { P[i * 4 + i] = qp->H[6 * N + i]; p[i] = qp->g[6 * N + i]; }
     for (int k = N - 1; k >= 0; --k) {
-        const double *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
-        const double *Hk = Hd + 6 * k, *gk = gd + 6 * k;
-        double pp[4], rt[2], qt[4];
+        const real *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
+        const real *Hk = Hd + 6 * k, *gk = gd + 6 * k;
+        real pp[4], rt[2], qt[4];
         if (factor) {
-            double Pb[4];
-            for (int i = 0; i < 4; ++i) { double a = 0; for (int j = 0; j < 4; ++j) a += P[i * 4 + j] * bb[j]; Pb[i] = a; }
+            real Pb[4];
+            for (int i = 0; i < 4; ++i) { real a = 0; for (int j = 0; j < 4; ++j) a += P[i * 4 + j] * bb[j]; Pb[i] = a; }
             memcpy(F->Pb[k], Pb, sizeof Pb);
         }
         for (int i = 0; i < 4; ++i) pp[i] = p[i] + F->Pb[k][i];
-        for (int i = 0; i < 2; ++i) { double a = gk[4 + i]; for (int j = 0; j < 4; ++j) a += B[j * 2 + i] * pp[j]; rt[i] = a; }
-        for (int i = 0; i < 4; ++i) { double a = gk[i]; for (int j = 0; j < 4; ++j) a += A[j * 4 + i] * pp[j]; qt[i] = a; }
+        for (int i = 0; i < 2; ++i) { real a = gk[4 + i]; for (int j = 0; j < 4; ++j) a += B[j * 2 + i] * pp[j]; rt[i] = a; }
+        for (int i = 0; i < 4; ++i) { real a = gk[i]; for (int j = 0; j < 4; ++j) a += A[j * 4 + i] * pp[j]; qt[i] = a; }
         if (factor) {
-            double PA[16], PB[8], Rt[4], St[8], Qt[16];
+            real PA[16], PB[8], Rt[4], St[8], Qt[16];
             for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j) { double a = 0; for (int m = 0; m < 4; ++m) a += P[i * 4 + m] * A[m * 4 + j]; PA[i * 4 + j] = a; }
+                for (int j = 0; j < 4; ++j) { real a = 0; for (int m = 0; m < 4; ++m) a += P[i * 4 + m] * A[m * 4 + j]; PA[i * 4 + j] = a; }
             for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 2; ++j) { double a = 0; for (int m = 0; m < 4; ++m) a += P[i * 4 + m] * B[m * 2 + j]; PB[i * 2 + j] = a; }
+                for (int j = 0; j < 2; ++j) { real a = 0; for (int m = 0; m < 4; ++m) a += P[i * 4 + m] * B[m * 2 + j]; PB[i * 2 + j] = a; }
             for (int i = 0; i < 2; ++i)
-                for (int j = 0; j < 2; ++j) { double a = (i == j) ? Hk[4 + i] : 0.0; for (int m = 0; m < 4; ++m) a += B[m * 2 + i] * PB[m * 2 + j]; Rt[i * 2 + j] = a; }
+                for (int j = 0; j < 2; ++j) { real a = (i == j) ? Hk[4 + i] : 0.0; for (int m = 0; m < 4; ++m) a += B[m * 2 + i] * PB[m * 2 + j]; Rt[i * 2 + j] = a; }
             for (int i = 0; i < 2; ++i)
-                for (int j = 0; j < 4; ++j) { double a = 0; for (int m = 0; m < 4; ++m) a += B[m * 2 + i] * PA[m * 4 + j]; St[i * 4 + j] = a; }
+                for (int j = 0; j < 4; ++j) { real a = 0; for (int m = 0; m < 4; ++m) a += B[m * 2 + i] * PA[m * 4 + j]; St[i * 4 + j] = a; }
             for (int i = 0; i < 4; ++i)
-                for (int j = 0; j < 4; ++j) { double a = (i == j) ? Hk[i] : 0.0; for (int m = 0; m < 4; ++m) a += A[m * 4 + i] * PA[m * 4 + j]; Qt[i * 4 + j] = a; }
+                for (int j = 0; j < 4; ++j) { real a = (i == j) ? Hk[i] : 0.0; for (int m = 0; m < 4; ++m) a += A[m * 4 + i] * PA[m * 4 + j]; Qt[i * 4 + j] = a; }
             /* symmetrise the 2x2 before inversion */
-            double rs = 0.5 * (Rt[1] + Rt[2]); Rt[1] = Rt[2] = rs;
+            real rs = 0.5 * (Rt[1] + Rt[2]); Rt[1] = Rt[2] = rs;
             inv2(Rt, F->Ri[k]);
             for (int i = 0; i < 2; ++i)
                 for (int j = 0; j < 4; ++j) F->K[k][i * 4 + j] = -(F->Ri[k][i * 2 + 0] * St[0 * 4 + j] + F->Ri[k][i * 2 + 1] * St[1 * 4 + j]);
             for (int i = 0; i < 4; ++i)
                 for (int j = 0; j < 4; ++j) P[i * 4 + j] = Qt[i * 4 + j] + St[0 * 4 + i] * F->K[k][0 * 4 + j] + St[1 * 4 + i] * F->K[k][1 * 4 + j];
             for (int i = 0; i < 4; ++i)
-                for (int j = i + 1; j < 4; ++j) { double s = 0.5 * (P[i * 4 + j] + P[j * 4 + i]); P[i * 4 + j] = P[j * 4 + i] = s; }
+                for (int j = i + 1; j < 4; ++j) { real s = 0.5 * (P[i * 4 + j] + P[j * 4 + i]); P[i * 4 + j] = P[j * 4 + i] = s; }
         }
         for (int i = 0; i < 2; ++i) F->kk[k][i] = -(F->Ri[k][i * 2 + 0] * rt[0] + F->Ri[k][i * 2 + 1] * rt[1]);
         for (int i = 0; i < 4; ++i) p[i] = qt[i] + F->K[k][0 * 4 + i] * rt[0] + F->K[k][1 * 4 + i] * rt[1];
     }
     /* forward */
-    double x[4];
+    real x[4];
     memcpy(x, qp->dx0, sizeof x);
     memcpy(dx, x, sizeof x);
     for (int k = 0; k < N; ++k) {
-        const double *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
-        double u[2];
-        for (int i = 0; i < 2; ++i) { double a = F->kk[k][i]; for (int j = 0; j < 4; ++j) a += F->K[k][i * 4 + j] * x[j]; u[i] = a; }
-        double xn[4];
+        const real *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
+        real u[2];
+        for (int i = 0; i < 2; ++i) { real a = F->kk[k][i]; for (int j = 0; j < 4; ++j) a += F->K[k][i * 4 + j] * x[j]; u[i] = a; }
+        real xn[4];
         for (int i = 0; i < 4; ++i) {
-            double a = bb[i];
+            real a = bb[i];
             for (int j = 0; j < 4; ++j) a += A[i * 4 + j] * x[j];
             for (int j = 0; j < 2; ++j) a += B[i * 2 + j] * u[j];
             xn[i] = a;
@@ -428,7 +457,7 @@ static void riccati(const or_qp *qp, const double *Hd, const double *gd, or_fact
     }
 }
 
-static inline double bnd_val(const double *dx, const double *du, int k, int j)
+static inline real bnd_val(const real *dx, const real *du, int k, int j)
 {
     return j == 0 ? dx[4 * k + 3] : du[2 * k + (j - 1)];
 }
@@ -438,23 +467,23 @@ static inline double bnd_val(const double *dx, const double *du, int k, int j)
  * 3 (infeasible: a fixed bounded component, the stage-0 s = x0's s, lies outside its bounds),
  * 4 (stall exit: the last iterate is returned as at the cap), 5 (diverged: mu reached
  * qp_mu_max or turned non-finite -- a QP failure, acados ACADOS_QP_FAILURE). */
-static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, double *work, int *nit_out)
+static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *F, real *work, int *nit_out)
 {
     int N = qp->N;
-    double *Hd = work, *gd = work + 6 * N, *dxn = work + 12 * N, *dun = dxn + 4 * (N + 1);
-    double *dta = dun + 2 * N, *dla = dta + 6 * N;
-    double *t = sol->t, *lam = sol->lam;
+    real *Hd = work, *gd = work + 6 * N, *dxn = work + 12 * N, *dun = dxn + 4 * (N + 1);
+    real *dta = dun + 2 * N, *dla = dta + 6 * N;
+    real *t = sol->t, *lam = sol->lam;
     int m = 0;
     /* Bound residual r = v - lo - t (resp. hi - v - t) of the infeasible start: nonzero where
      * the linearisation point is within t_min of a bound or beyond it.  Every update scales
      * all residuals by (1 - alpha), so max|r| = r0 * prod(1 - alpha) exactly. */
-    double r0 = 0.0, rscale = 1.0;
+    real r0 = 0.0, rscale = 1.0;
     for (int k = 0; k < N; ++k)
         for (int j = 0; j < 3; ++j) {
             for (int sd = 0; sd < 2; ++sd) {
                 int q = (k * 3 + j) * 2 + sd;
                 if (qp->act[k * 3 + j]) {
-                    double d = sd == 0 ? -qp->lo[k * 3 + j] : qp->hi[k * 3 + j];
+                    real d = sd == 0 ? -qp->lo[k * 3 + j] : qp->hi[k * 3 + j];
                     t[q] = d > o->t_min ? d : o->t_min;
                     lam[q] = o->mu0 / t[q];
                     if (t[q] - d > r0) r0 = t[q] - d;
@@ -467,15 +496,15 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     /* the stage-0 s is fixed (dx_0 = dx0): its bound is a feasibility check, not a variable */
     int infeasible = 0;
     if (qp->act[0]) {
-        double v = qp->dx0[3];
+        real v = qp->dx0[3];
         if (v < qp->lo[0] || v > qp->hi[0]) infeasible = 1;
     }
     /* start-point residuals of the stop test (z = 0, pi = 0): stationarity g + C' lam,
      * equality dx0 and the defects b */
-    double rg0 = 0.0, rb0 = 0.0;
+    real rg0 = 0.0, rb0 = 0.0;
     for (int k = 0; k < N; ++k) {
         for (int i = 0; i < 6; ++i) {
-            double r = qp->g[6 * k + i];
+            real r = qp->g[6 * k + i];
             int j = i == 3 ? 0 : (i >= 4 ? i - 3 : -1);
             if (j >= 0 && qp->act[k * 3 + j]) r += lam[(k * 3 + j) * 2 + 1] - lam[(k * 3 + j) * 2 + 0];
             if (fabs(r) > rg0) rg0 = fabs(r);
@@ -487,14 +516,14 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         if (fabs(qp->dx0[i]) > rb0) rb0 = fabs(qp->dx0[i]);
     }
 
-    double rs_stop = o->res_stop / r0;
+    real rs_stop = o->res_stop / r0;
     if (o->qp_tol_stat / rg0 < rs_stop) rs_stop = o->qp_tol_stat / rg0;
     if (o->qp_tol_eq / rb0 < rs_stop) rs_stop = o->qp_tol_eq / rb0;
     int nit = 0, converged = 0, stall = 0, stalled = 0, diverged = 0;
     for (int it = 0; it <= o->qp_iters && !infeasible; ++it) {
-        double mu = 0.0;
+        real mu = 0.0;
         for (int q = 0; q < 6 * N; ++q) mu += t[q] * lam[q];
-        mu /= (double)m;
+        mu /= (real)m;
         /* divergence (multipliers growing without bound; a NaN mu would pass the stop test) */
         if (!(mu < o->qp_mu_max)) { diverged = 1; break; }
         /* HPIPM's four exit residuals: complementarity, and the bound, stationarity and equality
@@ -507,19 +536,19 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
         if (it == o->qp_iters) break;   /* cap reached: tested once more above, no further step */
         nit++;
         for (int pass = 0; pass < 2; ++pass) {
-            double sigma_mu = 0.0;
+            real sigma_mu = 0.0;
             if (pass == 1) {
                 /* affine step length and centering parameter */
-                double amax = 1.0;
+                real amax = 1.0;
                 for (int q = 0; q < 6 * N; ++q) {
-                    if (dta[q] < 0.0) { double a = -t[q] / dta[q]; if (a < amax) amax = a; }
-                    if (dla[q] < 0.0) { double a = -lam[q] / dla[q]; if (a < amax) amax = a; }
+                    if (dta[q] < 0.0) { real a = -t[q] / dta[q]; if (a < amax) amax = a; }
+                    if (dla[q] < 0.0) { real a = -lam[q] / dla[q]; if (a < amax) amax = a; }
                 }
-                double mua = 0.0;
+                real mua = 0.0;
                 for (int q = 0; q < 6 * N; ++q) mua += (t[q] + amax * dta[q]) * (lam[q] + amax * dla[q]);
-                mua /= (double)m;
-                double r = mua / mu;
-                double sg = r * r * r;
+                mua /= (real)m;
+                real r = mua / mu;
+                real sg = r * r * r;
                 if (sg < o->sigma_min) sg = o->sigma_min;
                 sigma_mu = sg * mu;
             }
@@ -528,8 +557,8 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
                 for (int j = 0; j < 3; ++j) {
                     if (!qp->act[k * 3 + j]) continue;
                     int ql = (k * 3 + j) * 2, qh = ql + 1;
-                    double sl = lam[ql] / t[ql], sh = lam[qh] / t[qh];
-                    double cl = 0.0, ch = 0.0;
+                    real sl = lam[ql] / t[ql], sh = lam[qh] / t[qh];
+                    real cl = 0.0, ch = 0.0;
                     if (pass == 1) { cl = sigma_mu - dta[ql] * dla[ql]; ch = sigma_mu - dta[qh] * dla[qh]; }
                     Hd[6 * k + comp[j]] += sl + sh;
                     gd[6 * k + comp[j]] += -sl * qp->lo[k * 3 + j] - sh * qp->hi[k * 3 + j]
@@ -542,24 +571,24 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
                 for (int j = 0; j < 3; ++j) {
                     int ql = (k * 3 + j) * 2, qh = ql + 1;
                     if (!qp->act[k * 3 + j]) { dta[ql] = dta[qh] = dla[ql] = dla[qh] = 0.0; continue; }
-                    double v = bnd_val(dxn, dun, k, j);
-                    double sl = lam[ql] / t[ql], sh = lam[qh] / t[qh];
-                    double cl = 0.0, ch = 0.0;
+                    real v = bnd_val(dxn, dun, k, j);
+                    real sl = lam[ql] / t[ql], sh = lam[qh] / t[qh];
+                    real cl = 0.0, ch = 0.0;
                     if (pass == 1) { cl = sigma_mu - dta[ql] * dla[ql]; ch = sigma_mu - dta[qh] * dla[qh]; }
-                    double dtl = v - qp->lo[k * 3 + j] - t[ql];
-                    double dth = qp->hi[k * 3 + j] - v - t[qh];
+                    real dtl = v - qp->lo[k * 3 + j] - t[ql];
+                    real dth = qp->hi[k * 3 + j] - v - t[qh];
                     dta[ql] = dtl; dta[qh] = dth;
                     dla[ql] = cl / t[ql] - lam[ql] - sl * dtl;
                     dla[qh] = ch / t[qh] - lam[qh] - sh * dth;
                 }
         }
         /* step length with fraction to boundary */
-        double amax = 1.0 / o->frac;
+        real amax = 1.0 / o->frac;
         for (int q = 0; q < 6 * N; ++q) {
-            if (dta[q] < 0.0) { double a = -t[q] / dta[q]; if (a < amax) amax = a; }
-            if (dla[q] < 0.0) { double a = -lam[q] / dla[q]; if (a < amax) amax = a; }
+            if (dta[q] < 0.0) { real a = -t[q] / dta[q]; if (a < amax) amax = a; }
+            if (dla[q] < 0.0) { real a = -lam[q] / dla[q]; if (a < amax) amax = a; }
         }
-        double alpha = o->frac * amax;
+        real alpha = o->frac * amax;
         if (alpha > 1.0) alpha = 1.0;
         stall = alpha < o->qp_stall_alpha ? stall + 1 : 0;
         rscale *= 1.0 - alpha;
@@ -569,14 +598,14 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     }
     if (nit_out) *nit_out = nit;
     /* final state rollout from the damped controls */
-    double x[4];
+    real x[4];
     memcpy(x, qp->dx0, sizeof x);
     memcpy(sol->dx, x, sizeof x);
     for (int k = 0; k < N; ++k) {
-        const double *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
-        double xn[4];
+        const real *A = qp->A + 16 * k, *B = qp->B + 8 * k, *bb = qp->b + 4 * k;
+        real xn[4];
         for (int i = 0; i < 4; ++i) {
-            double a = bb[i];
+            real a = bb[i];
             for (int j = 0; j < 4; ++j) a += A[i * 4 + j] * x[j];
             for (int j = 0; j < 2; ++j) a += B[i * 2 + j] * sol->du[2 * k + j];
             xn[i] = a;
@@ -586,14 +615,14 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     }
     /* dynamics multipliers by the adjoint recursion:
      * pi_{N-1} = We dx_N + g_N ; pi_{k-1} = Hx dx_k + gx_k + A_k' pi_k + (lam_hi - lam_lo)_s */
-    double pi[4];
+    real pi[4];
     for (int i = 0; i < 4; ++i) pi[i] = qp->H[6 * N + i] * sol->dx[4 * N + i] + qp->g[6 * N + i];
     memcpy(sol->pi + 4 * (N - 1), pi, sizeof pi);
     for (int k = N - 1; k >= 1; --k) {
-        const double *A = qp->A + 16 * k;
-        double np[4];
+        const real *A = qp->A + 16 * k;
+        real np[4];
         for (int i = 0; i < 4; ++i) {
-            double a = qp->H[6 * k + i] * sol->dx[4 * k + i] + qp->g[6 * k + i];
+            real a = qp->H[6 * k + i] * sol->dx[4 * k + i] + qp->g[6 * k + i];
             for (int j = 0; j < 4; ++j) a += A[j * 4 + i] * pi[j];
             np[i] = a;
         }
@@ -603,9 +632,9 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
     }
     if (g_exp & 2) {
         for (int k = 0; k < N; ++k) {
-            const double *B = qp->B + 8 * k, *pk = sol->pi + 4 * k;
+            const real *B = qp->B + 8 * k, *pk = sol->pi + 4 * k;
             for (int i = 0; i < 2; ++i) {
-                double r = qp->H[6 * k + 4 + i] * sol->du[2 * k + i] + qp->g[6 * k + 4 + i];
+                real r = qp->H[6 * k + 4 + i] * sol->du[2 * k + i] + qp->g[6 * k + 4 + i];
                 for (int j = 0; j < 4; ++j) r += B[j * 2 + i] * pk[j];
                 const int q = (k * 3 + 1 + i) * 2;
                 lam[q + 1] = -r > 0.0 ? -r : 0.0;
@@ -613,28 +642,30 @@ static int qp_solve(const or_qp *qp, const or_opts *o, or_qp_sol *sol, or_fact *
             }
         }
     }
-    for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(sol->dx[q])) return 1;
-    for (int q = 0; q < 2 * N; ++q) if (!isfinite(sol->du[q])) return 1;
+    /* a QP whose mu turned non-finite diverged (5, as the kernel's QP_EXIT_DIVERGED, which it tests
+     * first): its solution is non-finite too, but it is a QP failure, not a status-1 breakdown */
     if (infeasible) return 3;
     if (diverged) return 5;
+    for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(sol->dx[q])) return 1;
+    for (int q = 0; q < 2 * N; ++q) if (!isfinite(sol->du[q])) return 1;
     return converged ? 0 : (stalled ? 4 : 2);
 }
 
 /* ================================================================ SQP */
 typedef struct {
-    double A[OR_MAX_N * 16], B[OR_MAX_N * 8], b[OR_MAX_N * 4];
-    double H[OR_MAX_N * 6 + 4], g[OR_MAX_N * 6 + 4];
-    double lo[OR_MAX_N * 3], hi[OR_MAX_N * 3];
+    real A[OR_MAX_N * 16], B[OR_MAX_N * 8], b[OR_MAX_N * 4];
+    real H[OR_MAX_N * 6 + 4], g[OR_MAX_N * 6 + 4];
+    real lo[OR_MAX_N * 3], hi[OR_MAX_N * 3];
     uint8_t act[OR_MAX_N * 3];
-    double dx[(OR_MAX_N + 1) * 4], du[OR_MAX_N * 2], pi[OR_MAX_N * 4];
-    double lam[OR_MAX_N * 6], t[OR_MAX_N * 6];
-    double work[OR_MAX_N * 40 + 64];
+    real dx[(OR_MAX_N + 1) * 4], du[OR_MAX_N * 2], pi[OR_MAX_N * 4];
+    real lam[OR_MAX_N * 6], t[OR_MAX_N * 6];
+    real work[OR_MAX_N * 40 + 64];
     or_fact F;
     int qp_total;
     int qp_capped;   /* QPs of this solve stopped by the iteration cap */
     int qp_stalled;  /* ... by the stall exit */
     int mode[OR_MAX_N];  /* motion-cone modes of the stages' RK4 evaluations (diagnostics) */
-    double kkt[18];  /* diagnostics of the last NLP KKT test (nlp_mode 1): see or_set_kkt_diag */
+    real kkt[18];  /* diagnostics of the last NLP KKT test (nlp_mode 1): see or_set_kkt_diag */
 } or_ws;
 
 /* KKT diagnostics (nlp_mode 1), per lane 18 doubles: the residuals of the last KKT test the SQP
@@ -645,38 +676,38 @@ typedef struct {
  * the term sum r_u' du of its u-stationarity residual r_u, -d'Hd, and sum pi'b - nu|b|; the number
  * of stages whose motion-cone modes (at the four RK4 evaluations) changed between the last two
  * linearisations, and over all linearisations from SQP iteration 10 on.  NULL: off. */
-static double *g_kkt_diag = NULL;
-void or_set_kkt_diag(double *buf) { g_kkt_diag = buf; }
+static real *g_kkt_diag = NULL;
+OR_EXPORT void or_set_kkt_diag(real *buf) { g_kkt_diag = buf; }
 
 
-static double ocp_cost(const or_opts *o, int N, const double *X, const double *U, const double *yref, const double *yref_e)
+static real ocp_cost(const or_opts *o, int N, const real *X, const real *U, const real *yref, const real *yref_e)
 {
-    double c = 0.0;
+    real c = 0.0;
     for (int k = 0; k < N; ++k) {
-        double s = 0.0;
-        for (int i = 0; i < 4; ++i) { double r = X[4 * k + i] - yref[6 * k + i]; s += o->W[i] * r * r; }
-        for (int i = 0; i < 2; ++i) { double r = U[2 * k + i] - yref[6 * k + 4 + i]; s += o->W[4 + i] * r * r; }
+        real s = 0.0;
+        for (int i = 0; i < 4; ++i) { real r = X[4 * k + i] - yref[6 * k + i]; s += o->W[i] * r * r; }
+        for (int i = 0; i < 2; ++i) { real r = U[2 * k + i] - yref[6 * k + 4 + i]; s += o->W[4 + i] * r * r; }
         c += 0.5 * o->tau * s;
     }
-    double s = 0.0;
-    for (int i = 0; i < 4; ++i) { double r = X[4 * N + i] - yref_e[i]; s += o->We[i] * r * r; }
+    real s = 0.0;
+    for (int i = 0; i < 4; ++i) { real r = X[4 * N + i] - yref_e[i]; s += o->We[i] * r * r; }
     return c + 0.5 * s;
 }
 
 /* Merit function for the line search (l1 exact penalty, Nocedal & Wright 18.2):
  * phi = J + sum_k nu_k' |phi(x_k,u_k) - x_{k+1}| + sum_bounds eta * violation */
-static double merit_eval(const or_shape *sh, const or_opts *o, const double *X, const double *U,
-                         const double *yref, const double *yref_e, const double *nu, const double *eta)
+static real merit_eval(const or_shape *sh, const or_opts *o, const real *X, const real *U,
+                         const real *yref, const real *yref_e, const real *nu, const real *eta)
 {
     int N = o->N;
-    double phi = ocp_cost(o, N, X, U, yref, yref_e);
+    real phi = ocp_cost(o, N, X, U, yref, yref_e);
     for (int k = 0; k < N; ++k) {
-        double xn[4], A[16], B[8];
+        real xn[4], A[16], B[8];
         rk4_sens(sh, o->Ts, X + 4 * k, U + 2 * k, xn, A, B);
         for (int i = 0; i < 4; ++i) phi += nu[4 * k + i] * fabs(xn[i] - X[4 * (k + 1) + i]);
-        double v[3] = {X[4 * k + 3], U[2 * k], U[2 * k + 1]};
+        real v[3] = {X[4 * k + 3], U[2 * k], U[2 * k + 1]};
         for (int j = (k == 0 && !o->stage0_s_bound ? 1 : 0); j < 3; ++j) {
-            double vl = o->lh[j] - v[j], vh = v[j] - o->uh[j];
+            real vl = o->lh[j] - v[j], vh = v[j] - o->uh[j];
             if (vl > 0) phi += eta[(3 * k + j) * 2 + 0] * vl;
             if (vh > 0) phi += eta[(3 * k + j) * 2 + 1] * vh;
         }
@@ -690,9 +721,9 @@ static double merit_eval(const or_shape *sh, const or_opts *o, const double *X, 
  *               merit backtracking with sufficient descent (alpha *= ls_alpha_red down
  *               to ls_alpha_min), damped multiplier update, at most sqp_iters QPs.
  * Returns status: 0 ok/converged, 1 NaN/Inf, 2 max iterations (mode 1). */
-static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
-                     const double *yref, const double *yref_e,
-                     double *X, double *U, double *PI, double *lam_out, int32_t *iters, or_ws *ws)
+static int sqp_solve(const or_shape *sh, const or_opts *o, const real x0[4],
+                     const real *yref, const real *yref_e,
+                     real *X, real *U, real *PI, real *lam_out, int32_t *iters, or_ws *ws)
 {
     int N = o->N;
     int status = 0;
@@ -700,12 +731,12 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
     qp.N = N; qp.A = ws->A; qp.B = ws->B; qp.b = ws->b; qp.H = ws->H; qp.g = ws->g;
     qp.lo = ws->lo; qp.hi = ws->hi; qp.act = ws->act;
     or_qp_sol sol = {ws->dx, ws->du, ws->pi, ws->lam, ws->t};
-    double LAM[OR_MAX_N * 6];
-    double nu[OR_MAX_N * 4], eta[OR_MAX_N * 6];
-    double Xt[(OR_MAX_N + 1) * 4], Ut[OR_MAX_N * 2];
-    memset(LAM, 0, sizeof(double) * 6 * N);
-    memset(nu, 0, sizeof(double) * 4 * N);
-    memset(eta, 0, sizeof(double) * 6 * N);
+    real LAM[OR_MAX_N * 6];
+    real nu[OR_MAX_N * 4], eta[OR_MAX_N * 6];
+    real Xt[(OR_MAX_N + 1) * 4], Ut[OR_MAX_N * 2];
+    memset(LAM, 0, sizeof(real) * 6 * N);
+    memset(nu, 0, sizeof(real) * 4 * N);
+    memset(eta, 0, sizeof(real) * 6 * N);
     int it;
     memset(ws->kkt, 0, sizeof ws->kkt);
     if (o->nlp_mode == 1) status = 2;
@@ -713,13 +744,13 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
      * infeasible and the solve stops before its first iteration (status 4, ACADOS_QP_FAILURE) */
     if (o->stage0_s_bound && !(x0[3] >= o->lh[0] && x0[3] <= o->uh[0])) {
         if (iters) *iters = 0;
-        if (lam_out) memset(lam_out, 0, sizeof(double) * 6 * N);
+        if (lam_out) memset(lam_out, 0, sizeof(real) * 6 * N);
         return 4;
     }
     for (it = 0; it < o->sqp_iters; ++it) {
         ws->kkt[16] = 0.0;
         for (int k = 0; k < N; ++k) {
-            double xn[4];
+            real xn[4];
             g_mode_code = 0;
             rk4_sens(sh, o->Ts, X + 4 * k, U + 2 * k, xn, ws->A + 16 * k, ws->B + 8 * k);
             if (it > 0 && g_mode_code != ws->mode[k]) {
@@ -736,7 +767,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 ws->H[6 * k + 4 + i] = o->tau * o->W[4 + i];
                 ws->g[6 * k + 4 + i] = o->tau * o->W[4 + i] * (U[2 * k + i] - yref[6 * k + 4 + i]);
             }
-            double v[3] = {X[4 * k + 3], U[2 * k], U[2 * k + 1]};
+            real v[3] = {X[4 * k + 3], U[2 * k], U[2 * k + 1]};
             for (int j = 0; j < 3; ++j) {
                 ws->lo[3 * k + j] = o->lh[j] - v[j];
                 ws->hi[3 * k + j] = o->uh[j] - v[j];
@@ -751,11 +782,11 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         if (o->nlp_mode == 1) {
             /* KKT residuals of the NLP at the current iterate */
             ws->kkt[2] = 0.0;
-            double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0, r_u = 0.0, r_x = 0.0;
+            real r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0, r_u = 0.0, r_x = 0.0;
             for (int k = 0; k < N; ++k) {
-                const double *A = ws->A + 16 * k, *B = ws->B + 8 * k, *pk = PI + 4 * k;
+                const real *A = ws->A + 16 * k, *B = ws->B + 8 * k, *pk = PI + 4 * k;
                 for (int i = 0; i < 2; ++i) {
-                    double r = ws->g[6 * k + 4 + i];
+                    real r = ws->g[6 * k + 4 + i];
                     for (int j = 0; j < 4; ++j) r += B[j * 2 + i] * pk[j];
                     r += LAM[(3 * k + 1 + i) * 2 + 1] - LAM[(3 * k + 1 + i) * 2 + 0];
                     if (fabs(r) > r_stat) r_stat = fabs(r);
@@ -763,7 +794,7 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 }
                 if (k >= 1) {
                     for (int i = 0; i < 4; ++i) {
-                        double r = ws->g[6 * k + i] - PI[4 * (k - 1) + i];
+                        real r = ws->g[6 * k + i] - PI[4 * (k - 1) + i];
                         for (int j = 0; j < 4; ++j) r += A[j * 4 + i] * pk[j];
                         if (i == 3) r += LAM[(3 * k) * 2 + 1] - LAM[(3 * k) * 2 + 0];
                         if (fabs(r) > r_stat) r_stat = fabs(r);
@@ -772,16 +803,16 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
                 }
                 for (int i = 0; i < 4; ++i) if (fabs(ws->b[4 * k + i]) > r_eq) r_eq = fabs(ws->b[4 * k + i]);
                 for (int j = (k == 0 && !o->stage0_s_bound ? 1 : 0); j < 3; ++j) {
-                    double sl = -ws->lo[3 * k + j], sh_ = ws->hi[3 * k + j];
+                    real sl = -ws->lo[3 * k + j], sh_ = ws->hi[3 * k + j];
                     if (-sl > r_ineq) r_ineq = -sl;
                     if (-sh_ > r_ineq) r_ineq = -sh_;
-                    double cl = fabs(LAM[(3 * k + j) * 2 + 0] * sl), ch = fabs(LAM[(3 * k + j) * 2 + 1] * sh_);
+                    real cl = fabs(LAM[(3 * k + j) * 2 + 0] * sl), ch = fabs(LAM[(3 * k + j) * 2 + 1] * sh_);
                     if (cl > r_comp) r_comp = cl;
                     if (ch > r_comp) r_comp = ch;
                 }
             }
             for (int i = 0; i < 4; ++i) {
-                double r = ws->g[6 * N + i] - PI[4 * (N - 1) + i];
+                real r = ws->g[6 * N + i] - PI[4 * (N - 1) + i];
                 if (fabs(r) > r_stat) r_stat = fabs(r);
                 if (fabs(r) > ws->kkt[2]) ws->kkt[2] = fabs(r);
             }
@@ -800,22 +831,22 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         /* non-finite QP solution: status 1; infeasible or diverged QP: status 4 (acados
          * ACADOS_QP_FAILURE); either way the SQP stops with its last finite iterate */
         if (qst == 1 || qst == 3 || qst == 5) { status = qst == 1 ? 1 : 4; break; }
-        double alpha = 1.0;
+        real alpha = 1.0;
         if (o->nlp_mode == 1) {
             /* merit weights (acados: max(|mult|, (weight + |mult|)/2)) */
             for (int q = 0; q < 4 * N; ++q) {
-                double a = fabs(ws->pi[q]);
-                double w = 0.5 * (nu[q] + a);
+                real a = fabs(ws->pi[q]);
+                real w = 0.5 * (nu[q] + a);
                 nu[q] = a > w ? a : w;
             }
             for (int q = 0; q < 6 * N; ++q) {
-                double a = fabs(ws->lam[q]);
-                double w = 0.5 * (eta[q] + a);
+                real a = fabs(ws->lam[q]);
+                real w = 0.5 * (eta[q] + a);
                 eta[q] = a > w ? a : w;
             }
-            double phi0 = merit_eval(sh, o, X, U, yref, yref_e, nu, eta);
+            real phi0 = merit_eval(sh, o, X, U, yref, yref_e, nu, eta);
             /* directional derivative  grad J' dw - sum nu|d| - sum eta viol (N&W 18.29) */
-            double dphi = 0.0;
+            real dphi = 0.0;
             for (int k = 0; k < N; ++k) {
                 for (int i = 0; i < 4; ++i) dphi += ws->g[6 * k + i] * ws->dx[4 * k + i];
                 for (int i = 0; i < 2; ++i) dphi += ws->g[6 * k + 4 + i] * ws->du[2 * k + i];
@@ -829,11 +860,11 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
             ws->kkt[8] = dphi;
             ws->kkt[9] = phi0;
             {
-                double ru = 0.0, dhd = 0.0, pb = 0.0;
+                real ru = 0.0, dhd = 0.0, pb = 0.0;
                 for (int k = 0; k < N; ++k) {
-                    const double *Bk = ws->B + 8 * k, *pk = ws->pi + 4 * k;
+                    const real *Bk = ws->B + 8 * k, *pk = ws->pi + 4 * k;
                     for (int i = 0; i < 2; ++i) {
-                        double r = ws->H[6 * k + 4 + i] * ws->du[2 * k + i] + ws->g[6 * k + 4 + i];
+                        real r = ws->H[6 * k + 4 + i] * ws->du[2 * k + i] + ws->g[6 * k + 4 + i];
                         for (int j = 0; j < 4; ++j) r += Bk[j * 2 + i] * pk[j];
                         r += ws->lam[(k * 3 + 1 + i) * 2 + 1] - ws->lam[(k * 3 + 1 + i) * 2 + 0];
                         ru += r * ws->du[2 * k + i];
@@ -850,10 +881,10 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
             for (;;) {
                 for (int q = 0; q < 4 * (N + 1); ++q) Xt[q] = X[q] + alpha * ws->dx[q];
                 for (int q = 0; q < 2 * N; ++q) Ut[q] = U[q] + alpha * ws->du[q];
-                double phi = merit_eval(sh, o, Xt, Ut, yref, yref_e, nu, eta);
+                real phi = merit_eval(sh, o, Xt, Ut, yref, yref_e, nu, eta);
                 ws->kkt[10] = phi;
                 if (phi <= phi0 + o->ls_eps * alpha * dphi) break;
-                double an = alpha * o->ls_alpha_red;
+                real an = alpha * o->ls_alpha_red;
                 if (an < ((g_exp & 4) ? 1e-12 : o->ls_alpha_min)) { ws->kkt[11] += 1.0; break; }   /* accept the last step tried */
                 alpha = an;
             }
@@ -861,20 +892,20 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const double x0[4],
         }
         for (int q = 0; q < 4 * (N + 1); ++q) X[q] += alpha * ws->dx[q];
         for (int q = 0; q < 2 * N; ++q) U[q] += alpha * ws->du[q];
-        const double ad = (g_exp & 1) ? 1.0 : alpha;
+        const real ad = (g_exp & 1) ? 1.0 : alpha;
         for (int q = 0; q < 4 * N; ++q) PI[q] += ad * (ws->pi[q] - PI[q]);
         for (int q = 0; q < 6 * N; ++q) LAM[q] += ad * (ws->lam[q] - LAM[q]);
     }
     if (iters) *iters = it;
-    if (lam_out) memcpy(lam_out, LAM, sizeof(double) * 6 * N);
+    if (lam_out) memcpy(lam_out, LAM, sizeof(real) * 6 * N);
     for (int q = 0; q < 4 * (N + 1); ++q) if (!isfinite(X[q])) status = 1;
     for (int q = 0; q < 2 * N; ++q) if (!isfinite(U[q])) status = 1;
     return status;
 }
 
 /* ================================================================ exported API */
-static void make_shape(or_shape *sh, const int32_t *n_ctrl, const double *ctrl, const double *knots,
-                       const double *params /* [b, c, mu] per shape */, int id, int max_ctrl)
+static void make_shape(or_shape *sh, const int32_t *n_ctrl, const real *ctrl, const real *knots,
+                       const real *params /* [b, c, mu] per shape */, int id, int max_ctrl)
 {
     sh->n = n_ctrl[id];
     sh->P = ctrl + (size_t)id * max_ctrl * 2;
@@ -888,9 +919,9 @@ static void make_shape(or_shape *sh, const int32_t *n_ctrl, const double *ctrl, 
  *   n_ctrl[n_shapes], ctrl[n_shapes][max_ctrl][2], knots[n_shapes][max_ctrl+4],
  *   params[n_shapes][3] = {b, c_ellipse, mu_sp} */
 
-int or_spline_eval(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-                   int max_ctrl, int32_t n, const int32_t *shape_id, const double *s,
-                   double *C, double *dC, double *D, double *dD, double *kappa)
+OR_EXPORT int or_spline_eval(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+                   int max_ctrl, int32_t n, const int32_t *shape_id, const real *s,
+                   real *C, real *dC, real *D, real *dD, real *kappa)
 {
     for (int32_t i = 0; i < n; ++i) {
         or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
@@ -901,9 +932,9 @@ int or_spline_eval(const int32_t *n_ctrl, const double *ctrl, const double *knot
     return 0;
 }
 
-int or_dynamics(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-                int max_ctrl, int32_t n, const int32_t *shape_id, const double *x, const double *u,
-                double *f, double *J)
+OR_EXPORT int or_dynamics(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+                int max_ctrl, int32_t n, const int32_t *shape_id, const real *x, const real *u,
+                real *f, real *J)
 {
     #pragma omp parallel for schedule(static)
     for (int32_t i = 0; i < n; ++i) {
@@ -913,9 +944,9 @@ int or_dynamics(const int32_t *n_ctrl, const double *ctrl, const double *knots, 
     return 0;
 }
 
-int or_rk4(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-           int max_ctrl, int32_t n, const int32_t *shape_id, double h, const double *x, const double *u,
-           double *xn, double *A, double *B)
+OR_EXPORT int or_rk4(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+           int max_ctrl, int32_t n, const int32_t *shape_id, real h, const real *x, const real *u,
+           real *xn, real *A, real *B)
 {
     g_probe_eps = 0.0;
     #pragma omp parallel for schedule(static)
@@ -926,8 +957,8 @@ int or_rk4(const int32_t *n_ctrl, const double *ctrl, const double *knots, const
     return 0;
 }
 
-int or_vbound(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-              int max_ctrl, const or_opts *o, int32_t n, const int32_t *shape_id, const double *s, double *vb)
+OR_EXPORT int or_vbound(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+              int max_ctrl, const or_opts *o, int32_t n, const int32_t *shape_id, const real *s, real *vb)
 {
     for (int32_t i = 0; i < n; ++i) {
         or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
@@ -939,9 +970,9 @@ int or_vbound(const int32_t *n_ctrl, const double *ctrl, const double *knots, co
 /* Batched QP solve (for QP-level parity).  Per lane: A (N x16), B (N x 8), b (N x 4),
  * H (6N+4), g (6N+4), lo/hi (N x 3), act (N x 3), dx0 (4).
  * Outputs dx ((N+1)x4), du (N x 2), pi (N x 4), lam (N x 6). */
-int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, const double *b,
-                const double *H, const double *g, const double *lo, const double *hi, const uint8_t *act,
-                const double *dx0, double *dx, double *du, double *pi, double *lam, int32_t *iters,
+OR_EXPORT int or_qp_batch(const or_opts *o, int32_t nb, const real *A, const real *B, const real *b,
+                const real *H, const real *g, const real *lo, const real *hi, const uint8_t *act,
+                const real *dx0, real *dx, real *du, real *pi, real *lam, int32_t *iters,
                 int32_t *qp_status /* optional: 0 converged, 1 non-finite, 2 capped, 3 infeasible */)
 {
     int N = o->N;
@@ -975,11 +1006,11 @@ int or_qp_batch(const or_opts *o, int32_t nb, const double *A, const double *B, 
 /* Batched OCP solve (acados ocp.solve() level): initial guess X,U,PI in/out.
  * x0: B x 4, yref: B x N x 6, yref_e: B x 4, X: B x (N+1) x 4, U: B x N x 2, PI: B x N x 4.
  * status, cost: B. */
-int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
+OR_EXPORT int or_ocp_solve(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
                  int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
-                 const double *x0, const double *yref, const double *yref_e,
-                 double *X, double *U, double *PI, double *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
-                 double *cost, int nthreads, int32_t *qp_capped, int32_t *qp_stalled)
+                 const real *x0, const real *yref, const real *yref_e,
+                 real *X, real *U, real *PI, real *lam, int32_t *status, int32_t *iters, int32_t *qp_iter,
+                 real *cost, int nthreads, int32_t *qp_capped, int32_t *qp_stalled)
 {
     g_probe_eps = o->model_probe;
     g_probe_seed = (uint64_t)(uint32_t)o->probe_seed;
@@ -994,8 +1025,8 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
         #pragma omp for schedule(dynamic, 1)
         for (int32_t i = 0; i < nb; ++i) {
             or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
-            double *Xi = X + (size_t)i * 4 * (N + 1), *Ui = U + (size_t)i * 2 * N, *Pi = PI + (size_t)i * 4 * N;
-            const double *yr = yref + (size_t)i * 6 * N, *ye = yref_e + (size_t)i * 4;
+            real *Xi = X + (size_t)i * 4 * (N + 1), *Ui = U + (size_t)i * 2 * N, *Pi = PI + (size_t)i * 4 * N;
+            const real *yr = yref + (size_t)i * 6 * N, *ye = yref_e + (size_t)i * 4;
             ws->qp_total = 0;
             ws->qp_capped = 0;
             ws->qp_stalled = 0;
@@ -1015,7 +1046,7 @@ int or_ocp_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots,
  * (NMPC_controller.m:425-431): D = delay_buff_comp zero columns prepended to the T columns of
  * traj, whose u_t-reference row (6) copies the first real column; get_y_ref (:307-313) clamps
  * an index past the end to the last column. */
-static void ref_column(const double *traj, int32_t T, int32_t D, int c, double out[6])
+static void ref_column(const real *traj, int32_t T, int32_t D, int c, real out[6])
 {
     if (c > T + D) c = T + D;
     if (c < 1) c = 1;
@@ -1030,15 +1061,15 @@ static void ref_column(const double *traj, int32_t T, int32_t D, int c, double o
 /* One NMPC_controller.solve(x0, index_time) (NMPC_controller.m:329-423) on one lane.  Warm start
  * X/U/PI + warm_valid in/out (shifted on return, :397-399); returns the status; u0 = U(:,1) of the
  * unshifted solution (:403). */
-static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0_in[4], const double *traj,
-                           int32_t T, int32_t D, int32_t index_time, double *X, double *U, double *PI,
-                           uint8_t *warm_valid, double u0[2], int32_t *iters, int32_t *qp_iter, int32_t *qp_capped,
-                           double *cost, or_ws *ws, int32_t *qp_stalled)
+static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const real x0_in[4], const real *traj,
+                           int32_t T, int32_t D, int32_t index_time, real *X, real *U, real *PI,
+                           uint8_t *warm_valid, real u0[2], int32_t *iters, int32_t *qp_iter, int32_t *qp_capped,
+                           real *cost, or_ws *ws, int32_t *qp_stalled)
 {
     int N = o->N;
     if (N < 1 || N > OR_MAX_N) return 1;
-    double yref[OR_MAX_N * 6], ye[4];
-    double x0[4];
+    real yref[OR_MAX_N * 6], ye[4];
+    real x0[4];
     memcpy(x0, x0_in, sizeof x0);
     /* :332 pre-wrap of s into [-b, b) */
     x0[3] = mat_mod(x0[3], sh->b) - sh->b * (x0[3] < 0.0 ? 1.0 : 0.0);
@@ -1052,22 +1083,22 @@ static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0
         for (int q = 0; q < 4 * N; ++q) PI[q] = 0.0;
     }
     /* :357-364 clip first control */
-    double vb = v_bound(sh, o, x0[3]);
+    real vb = v_bound(sh, o, x0[3]);
     if (fabs(U[1]) > vb) {
-        double ut_old = U[1];
+        real ut_old = U[1];
         U[1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
         U[0] = U[1] * U[0] / ut_old;
     }
     /* :366-380 Euler warm-start rollout with per-stage clip */
     memcpy(X, x0, sizeof x0);
     for (int j = 1; j <= N; ++j) {
-        double f[4];
+        real f[4];
         dynamics(sh, X + 4 * (j - 1), U + 2 * (j - 1), f, NULL);
         for (int c = 0; c < 4; ++c) X[4 * j + c] = X[4 * (j - 1) + c] + o->Ts * f[c];
         vb = v_bound(sh, o, X[4 * j + 3]);
         if (j == N) break;
         if (fabs(U[2 * j + 1]) > vb) {
-            double ut_old = U[2 * j + 1];
+            real ut_old = U[2 * j + 1];
             U[2 * j + 1] = (ut_old > 0 ? 1.0 : (ut_old < 0 ? -1.0 : 0.0)) * vb;
             U[2 * j] = U[2 * j + 1] * U[2 * j] / ut_old;
         }
@@ -1083,9 +1114,9 @@ static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0
     if (cost) *cost = ocp_cost(o, N, X, U, yref, ye);
     u0[0] = U[0]; u0[1] = U[1];
     /* :397-399 shift (duplicate last column) */
-    memmove(U, U + 2, sizeof(double) * 2 * (N - 1));
-    memmove(X, X + 4, sizeof(double) * 4 * N);
-    memmove(PI, PI + 4, sizeof(double) * 4 * (N - 1));
+    memmove(U, U + 2, sizeof(real) * 2 * (N - 1));
+    memmove(X, X + 4, sizeof(real) * 4 * N);
+    memmove(PI, PI + 4, sizeof(real) * 4 * (N - 1));
     *warm_valid = 1;
     return status;
 }
@@ -1096,11 +1127,11 @@ static int ctrl_solve_lane(const or_shape *sh, const or_opts *o, const double x0
  * index_time: B (1-based, as in MATLAB).  Warm start Xw/Uw/PIw: B x ... in/out,
  * warm_valid: B flags (0 = cold start, :351-355); on return they hold the SHIFTED
  * solution (:397-399) and warm_valid = 1.  u0: B x 2 (the unshifted U(:,1), :403). */
-int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
+OR_EXPORT int or_controller_solve(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
                         int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id,
-                        const double *x0_in, const double *traj, int32_t T, const int32_t *index_time,
-                        double *Xw, double *Uw, double *PIw, uint8_t *warm_valid,
-                        double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost, int nthreads,
+                        const real *x0_in, const real *traj, int32_t T, const int32_t *index_time,
+                        real *Xw, real *Uw, real *PIw, uint8_t *warm_valid,
+                        real *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, real *cost, int nthreads,
                         int32_t *qp_capped, int32_t delay_cols, int32_t *qp_stalled)
 {
     g_probe_eps = o->model_probe;
@@ -1132,31 +1163,31 @@ int or_controller_solve(const int32_t *n_ctrl, const double *ctrl, const double 
  * reference, whose iterates cannot be reproduced: restated as a damped Newton iteration on the
  * periodic spline, C evaluated at the floor-mod of s as evalSpline does, bspline_shape.m:192-199;
  * it converges to the local minimum of the start point's basin). */
-static double phi_contact(const or_shape *sh, double s, double px, double py)
+static real phi_contact(const or_shape *sh, real s, real px, real py)
 {
-    double C[2], dC[2];
+    real C[2], dC[2];
     spline_C(sh, mat_mod(s, sh->b), C, dC);
     return (C[0] - px) * (C[0] - px) + (C[1] - py) * (C[1] - py);
 }
 
-static double reproject_contact(const or_shape *sh, double px, double py, double s0)
+static real reproject_contact(const or_shape *sh, real px, real py, real s0)
 {
-    double s = s0, phi = phi_contact(sh, s, px, py);
+    real s = s0, phi = phi_contact(sh, s, px, py);
     for (int it = 0; it < 60; ++it) {
-        double C[2], dC[2], D[2], dD[2];
-        const double sw = mat_mod(s, sh->b);
+        real C[2], dC[2], D[2], dD[2];
+        const real sw = mat_mod(s, sh->b);
         spline_C(sh, sw, C, dC);
         spline_Cdot(sh, sw, D, dD);
-        const double ex = C[0] - px, ey = C[1] - py;
-        const double g = 2.0 * (ex * dC[0] + ey * dC[1]);
-        const double h = 2.0 * (dC[0] * dC[0] + dC[1] * dC[1] + ex * dD[0] + ey * dD[1]);
+        const real ex = C[0] - px, ey = C[1] - py;
+        const real g = 2.0 * (ex * dC[0] + ey * dC[1]);
+        const real h = 2.0 * (dC[0] * dC[0] + dC[1] * dC[1] + ex * dD[0] + ey * dD[1]);
         if (fabs(g) < 1e-14) break;
-        double step = h > 0.0 ? -g / h : (g > 0.0 ? -0.05 : 0.05) * sh->b;
-        const double smax = 0.25 * sh->b;
+        real step = h > 0.0 ? -g / h : (g > 0.0 ? -0.05 : 0.05) * sh->b;
+        const real smax = 0.25 * sh->b;
         if (step > smax) step = smax;
         if (step < -smax) step = -smax;
         int ok = 0;
-        double sn = s, phin = phi;
+        real sn = s, phin = phi;
         for (int k = 0; k < 60; ++k) {
             sn = s + step;
             phin = phi_contact(sh, sn, px, py);
@@ -1179,11 +1210,11 @@ static double reproject_contact(const or_shape *sh, double px, double py, double
  * > 0 the plant applies its buffered input (helper.m:289-296).  Cold start; both buffers start at
  * zero.  Outputs: Xtraj nb x (n+1) x 4 (states after disturbance and noise), Xsim nb x n x 4 (the
  * predicted states handed to the solver; optional), Utraj nb x n x 2, Straj nb x n (status). */
-int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-                   int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id, const double *x0_in,
-                   const double *traj, int32_t T, const int32_t *index0, int32_t n_steps, const double *noise,
-                   int32_t delay_cols, int32_t plant_delay_cols, int32_t dist_step, const double *dist_amp,
-                   const double *xwidth, double *Xtraj, double *Xsim, double *Utraj, int32_t *Straj, int nthreads)
+OR_EXPORT int or_closed_loop(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+                   int max_ctrl, const or_opts *o, int32_t nb, const int32_t *shape_id, const real *x0_in,
+                   const real *traj, int32_t T, const int32_t *index0, int32_t n_steps, const real *noise,
+                   int32_t delay_cols, int32_t plant_delay_cols, int32_t dist_step, const real *dist_amp,
+                   const real *xwidth, real *Xtraj, real *Xsim, real *Utraj, int32_t *Straj, int nthreads)
 {
     g_probe_eps = o->model_probe;
     g_probe_seed = (uint64_t)(uint32_t)o->probe_seed;
@@ -1195,54 +1226,54 @@ int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
     #pragma omp parallel
     {
         or_ws *ws = (or_ws *)malloc(sizeof(or_ws));
-        double *X = (double *)malloc(sizeof(double) * 4 * (N + 1)), *U = (double *)malloc(sizeof(double) * 2 * N);
-        double *PI = (double *)malloc(sizeof(double) * 4 * N);
-        double *ubc = (double *)calloc(2 * (size_t)(delay_cols + 1), sizeof(double));
-        double *ubp = (double *)calloc(2 * (size_t)(plant_delay_cols + 1), sizeof(double));
+        real *X = (real *)malloc(sizeof(real) * 4 * (N + 1)), *U = (real *)malloc(sizeof(real) * 2 * N);
+        real *PI = (real *)malloc(sizeof(real) * 4 * N);
+        real *ubc = (real *)calloc(2 * (size_t)(delay_cols + 1), sizeof(real));
+        real *ubp = (real *)calloc(2 * (size_t)(plant_delay_cols + 1), sizeof(real));
         #pragma omp for schedule(dynamic, 1)
         for (int32_t i = 0; i < nb; ++i) {
             or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
             uint8_t valid = 0;
-            memset(ubc, 0, sizeof(double) * 2 * (size_t)(delay_cols + 1));
-            memset(ubp, 0, sizeof(double) * 2 * (size_t)(plant_delay_cols + 1));
-            double x[4];
+            memset(ubc, 0, sizeof(real) * 2 * (size_t)(delay_cols + 1));
+            memset(ubp, 0, sizeof(real) * 2 * (size_t)(plant_delay_cols + 1));
+            real x[4];
             memcpy(x, x0_in + 4 * i, sizeof x);
-            double s0_spline = 0.0;
+            real s0_spline = 0.0;
             for (int32_t t = 0; t < n_steps; ++t) {
                 if (dist_step > 0 && t + 1 == dist_step) {
                     x[1] += dist_amp[i];
-                    double C[2], dC[2];
+                    real C[2], dC[2];
                     spline_C(&sh, mat_mod(x[3], sh.b), C, dC);
-                    const double s = reproject_contact(&sh, -0.5 * xwidth[shape_id[i]], C[1] - dist_amp[i], s0_spline);
+                    const real s = reproject_contact(&sh, -0.5 * xwidth[shape_id[i]], C[1] - dist_amp[i], s0_spline);
                     s0_spline = mat_mod(s, sh.b) - sh.b * (s < 0.0 ? 1.0 : 0.0);
                     x[3] = s0_spline;
                 }
                 if (noise)
                     for (int c = 0; c < 4; ++c) x[c] += noise[((size_t)t * nb + i) * 4 + c];
                 memcpy(Xtraj + ((size_t)i * (n_steps + 1) + t) * 4, x, sizeof x);
-                double xs[4];
+                real xs[4];
                 memcpy(xs, x, sizeof xs);
                 for (int k = 1; k <= delay_cols; ++k) {       /* u_buff_contr(:, end-k+1): oldest first */
-                    double f[4];
+                    real f[4];
                     dynamics(&sh, xs, ubc + 2 * (delay_cols - k), f, NULL);
                     for (int c = 0; c < 4; ++c) xs[c] += o->Ts * f[c];
                 }
                 if (Xsim) memcpy(Xsim + ((size_t)i * n_steps + t) * 4, xs, sizeof xs);
-                double u[2];
+                real u[2];
                 const int st = ctrl_solve_lane(&sh, o, xs, traj, T, delay_cols, index0[i] + t + delay_cols, X, U, PI,
                                                &valid, u, NULL, NULL, NULL, NULL, ws, NULL);
                 if (delay_cols > 0) {                         /* u_buff_contr = [u, u_buff_contr(:, 1:end-1)] */
-                    memmove(ubc + 2, ubc, sizeof(double) * 2 * (size_t)(delay_cols - 1));
+                    memmove(ubc + 2, ubc, sizeof(real) * 2 * (size_t)(delay_cols - 1));
                     ubc[0] = u[0]; ubc[1] = u[1];
                 }
                 memcpy(Utraj + ((size_t)i * n_steps + t) * 2, u, sizeof u);
                 if (Straj) Straj[(size_t)i * n_steps + t] = st;
-                double f[4];
+                real f[4];
                 if (plant_delay_cols == 0) {
                     dynamics(&sh, x, u, f, NULL);
                 } else {                                      /* u_buff_plant(:, end), then push */
                     dynamics(&sh, x, ubp + 2 * (plant_delay_cols - 1), f, NULL);
-                    memmove(ubp + 2, ubp, sizeof(double) * 2 * (size_t)(plant_delay_cols - 1));
+                    memmove(ubp + 2, ubp, sizeof(real) * 2 * (size_t)(plant_delay_cols - 1));
                     ubp[0] = u[0]; ubp[1] = u[1];
                 }
                 for (int c = 0; c < 4; ++c) x[c] += o->Ts * f[c];
@@ -1255,9 +1286,9 @@ int or_closed_loop(const int32_t *n_ctrl, const double *ctrl, const double *knot
 }
 
 /* contact re-projection alone (building block for the tests) */
-int or_reproject_contact(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params,
-                         int max_ctrl, int32_t n, const int32_t *shape_id, const double *px, const double *py,
-                         const double *s0, double *s)
+OR_EXPORT int or_reproject_contact(const int32_t *n_ctrl, const real *ctrl, const real *knots, const real *params,
+                         int max_ctrl, int32_t n, const int32_t *shape_id, const real *px, const real *py,
+                         const real *s0, real *s)
 {
     for (int32_t i = 0; i < n; ++i) {
         or_shape sh; make_shape(&sh, n_ctrl, ctrl, knots, params, shape_id[i], max_ctrl);
@@ -1266,4 +1297,46 @@ int or_reproject_contact(const int32_t *n_ctrl, const double *ctrl, const double
     return 0;
 }
 
-int or_max_n(void) { return OR_MAX_N; }
+OR_EXPORT int or_max_n(void) { return OR_MAX_N; }
+
+#ifdef OR_EXT
+/* orx_controller_solve: or_controller_solve in the extended scalar type, double in/out (inputs
+ * converted exactly; outputs rounded once).  Shapes: n_shapes entries of the usual table layout.
+ * No model probe, no diagnostics. */
+#if OR_EXT == 2
+#define ORX_NAME orx_controller_solve_q
+#else
+#define ORX_NAME orx_controller_solve_l
+#endif
+static real *to_real(const double *a, size_t n)
+{
+    real *r = (real *)malloc(sizeof(real) * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) r[i] = a[i];
+    return r;
+}
+static void from_real(double *a, const real *r, size_t n) { for (size_t i = 0; i < n; ++i) a[i] = (double)r[i]; }
+
+int ORX_NAME(const int32_t *n_ctrl, const double *ctrl, const double *knots, const double *params, int max_ctrl,
+             int32_t n_shapes, const or_opts *o, int32_t nb, const int32_t *shape_id, const double *x0_in,
+             const double *traj, int32_t T, const int32_t *index_time, double *Xw, double *Uw, double *PIw,
+             uint8_t *warm_valid, double *u0, int32_t *status, int32_t *iters, int32_t *qp_iter, double *cost,
+             int nthreads, int32_t delay_cols)
+{
+    if (o->model_probe != 0.0) return -1;
+    const int N = o->N;
+    const size_t ns = (size_t)n_shapes, nbs = (size_t)nb;
+    real *c = to_real(ctrl, ns * max_ctrl * 2), *k = to_real(knots, ns * (max_ctrl + 4)), *pr = to_real(params, ns * 3);
+    real *x0 = to_real(x0_in, nbs * 4), *tr = to_real(traj, (size_t)T * 6);
+    real *X = to_real(Xw, nbs * 4 * (N + 1)), *U = to_real(Uw, nbs * 2 * N), *P = to_real(PIw, nbs * 4 * N);
+    real *u = (real *)calloc(nbs * 2 + 1, sizeof(real)), *cs = (real *)calloc(nbs + 1, sizeof(real));
+    const int r = or_controller_solve(n_ctrl, c, k, pr, max_ctrl, o, nb, shape_id, x0, tr, T, index_time, X, U, P,
+                                      warm_valid, u, status, iters, qp_iter, cs, nthreads, NULL, delay_cols, NULL);
+    from_real(Xw, X, nbs * 4 * (N + 1));
+    from_real(Uw, U, nbs * 2 * N);
+    from_real(PIw, P, nbs * 4 * N);
+    from_real(u0, u, nbs * 2);
+    from_real(cost, cs, nbs);
+    free(c); free(k); free(pr); free(x0); free(tr); free(X); free(U); free(P); free(u); free(cs);
+    return r;
+}
+#endif

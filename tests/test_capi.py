@@ -71,6 +71,19 @@ def test_default_options_and_validation():
     assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
     assert b"N and batch" in L.qsp_last_error()
     assert L.qsp_solve(None) == -1
+    # ABI v2 guards: a caller built against another header (struct_size), the divergence cap
+    bad.batch = 1
+    for size in (C.sizeof(_lib.Options) - 8, C.sizeof(_lib.Options) + 8, 0):
+        bad.struct_size = size
+        assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+        assert b"struct_size" in L.qsp_last_error()
+    bad.struct_size = C.sizeof(_lib.Options)
+    for mu_max in (0.0, -1.0, float("nan")):
+        bad.qp_mu_max = mu_max
+        assert L.qsp_create(C.byref(bad), C.byref(h)) == -1
+        assert b"qp_mu_max" in L.qsp_last_error()
+    res = np.zeros(4)
+    assert L.qsp_get_residuals(None, res.ctypes.data_as(C.c_void_p)) == -1
 
 
 def test_shape_from_ply_matches_oracle_bitwise():

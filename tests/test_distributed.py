@@ -99,3 +99,55 @@ def test_bench_gpus_flag_launches_ranks_or_fails_loudly():
         pytest.skip("GPUs visible: the launch itself is tests/test_gpu_multirank.py's")
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "GPU(s) visible" in r.stderr
+
+
+class _MockNccl:
+    """Stands in for torch.distributed on the nccl (RCCL) backend for gather_lanes: checks what RCCL
+    requires of an all_gather -- one output per rank, every tensor of the input's shape, dtype and
+    device, the input not moved off its device -- and delivers the ranks' padded shards."""
+
+    def __init__(self, world, pads=None):
+        self.world, self.pads, self.seen = world, pads, []
+
+    def all_gather(self, parts, pad):
+        assert len(parts) == self.world
+        for p in parts:
+            assert p.shape == pad.shape and p.dtype == pad.dtype and p.device == pad.device
+        self.seen.append((tuple(pad.shape), pad.dtype, pad.device))
+        if self.pads is not None:
+            for p, q in zip(parts, self.pads):
+                p.copy_(q)
+
+
+@pytest.mark.parametrize("world,total", [(8, 262144), (8, 262147), (2, 5)])
+@pytest.mark.parametrize("dtype", ["float64", "int32"])
+def test_gather_lanes_nccl_branch_shapes(world, total, dtype):
+    """bench.py's gather on the nccl backend hands gather_lanes device tensors (d_u0 B x 2 FP64, d_st B
+    int32, red_dev = the rank's GPU).  Without a GPU here: the same call on 'meta' tensors (device
+    tensors that hold no data) must build padded buffers of the largest shard's shape, dtype and
+    device -- so the first 8-GPU run cannot fail on this branch -- and, on CPU tensors with a mock
+    collective, reassemble the global lane order exactly (unequal shards at 262 147 lanes)."""
+    import torch
+    from uclv_qs_pushing_matlab_amd.sharding import gather_lanes
+    dt = getattr(torch, dtype)
+    cap = max(h - l for l, h in (shard_range(total, world, r) for r in range(world)))
+    tail = (2,) if dtype == "float64" else ()
+    for rank in range(world):
+        lo, hi = shard_range(total, world, rank)
+        m = _MockNccl(world)
+        out = gather_lanes(torch.empty((hi - lo,) + tail, dtype=dt, device="meta"), total, m, world, rank)
+        assert m.seen == [((cap,) + tail, dt, torch.device("meta"))]
+        assert out.shape == (total,) + tail and out.dtype == dt and out.device.type == "meta"
+    full = torch.arange(total * (2 if tail else 1), dtype=dt).reshape((total,) + tail)
+    pads = []
+    for r in range(world):
+        lo, hi = shard_range(total, world, r)
+        p = torch.zeros((cap,) + tail, dtype=dt)
+        p[: hi - lo] = full[lo:hi]
+        pads.append(p)
+    for rank in (0, world - 1):
+        lo, hi = shard_range(total, world, rank)
+        out = gather_lanes(full[lo:hi].clone(), total, _MockNccl(world, pads), world, rank)
+        assert torch.equal(out, full)
+    with pytest.raises(ValueError):
+        gather_lanes(torch.empty((cap + 1,) + tail, dtype=dt), total, _MockNccl(world), world, 0)

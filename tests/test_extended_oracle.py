@@ -1,0 +1,67 @@
+"""The extended-precision literal oracle (oracle/qsp_oracle.c built with OR_EXT: long double and
+__float128) and the adjudication it makes of the formulation disagreements.
+
+Where the kernel-order twin (= the GPU, bit for bit) and the double literal restatement disagree on
+u0 by more than 1e-6, the same literal formulas evaluated in __float128 give the answer of exact
+arithmetic as far as the SQP's amplification allows (long double agreeing with quad to 1e-6 says it
+does).  tests/tools/ext_adjudicate.py scanned the bench sample (the first 5 904 lanes of the configs[2]
+workload) and stored every disagreeing lane that is probe-stable in the literal or in both
+implementations (tests/golden/ext_adjudication_c2.json); this test recomputes them.  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+NAMES = ("santal", "balea", "montana", "pulirapid")
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle.oracle import Oracle
+    return Oracle(NAMES)
+
+
+def test_extended_builds_agree_on_a_benign_solve(orc):
+    """One SQP-RTI iteration per call (no chaos can build up): double, long double and __float128
+    literal restatements agree to rounding, and the extended ones are closer to each other."""
+    from bench import SEED, make_inputs
+    from oracle.oracle import make_opts
+    x0, _, _, sid, traj = make_inputs(16, 20, SEED)
+    op = make_opts(N=20, sqp_iters=1)
+    u = {p: orc.controller_solve_ext(op, x0, traj, 1, orc.new_warm(16, 20), shape_id=sid, precision=p)["u0"]
+         for p in ("long", "quad")}
+    ud = orc.controller_solve(op, x0, traj, 1, orc.new_warm(16, 20), shape_id=sid)["u0"]
+    assert np.abs(ud - u["quad"]).max() < 1e-11
+    assert np.abs(u["long"] - u["quad"]).max() < 1e-14
+    assert np.abs(u["long"] - u["quad"]).max() <= np.abs(ud - u["quad"]).max()
+
+
+def test_adjudicated_lanes_config2(orc):
+    from bench import SEED, make_inputs
+    from oracle.oracle import Oracle, make_opts
+    g = json.load(open(os.path.join(GOLDEN, "ext_adjudication_c2.json")))
+    s = g["summary"]
+    # the scan: 560 of 5 904 lanes disagree by > 1e-6; in exact arithmetic (quad) the twin and the
+    # literal are right about equally often on them, and on the one lane stable under every probe
+    # in both implementations the extended-precision answer is the twin's (the GPU's)
+    assert s["disagreeing_lanes"] == 560 and s["lanes"] == 5904
+    assert abs(s["all_disagreeing"]["twin"] - s["all_disagreeing"]["literal"]) <= 10
+    assert s["disagreeing_stable_in_both"] == {"twin": 1, "literal": 0, "both": 0, "neither": 0}
+    lanes = np.array([l["lane"] for l in g["lanes"]])
+    x0, _, _, sid, traj = make_inputs(65536, 20, SEED)
+    x0, sid = x0[lanes], sid[lanes]
+    op = make_opts(N=20, sqp_iters=50)
+    n = len(lanes)
+    u_tw = Oracle(NAMES, twin=True).controller_solve(op, x0, traj, 1, orc.new_warm(n, 20), shape_id=sid)["u0"]
+    u_lit = orc.controller_solve(op, x0, traj, 1, orc.new_warm(n, 20), shape_id=sid)["u0"]
+    u_q = orc.controller_solve_ext(op, x0, traj, 1, orc.new_warm(n, 20), shape_id=sid, precision="quad")["u0"]
+    for j, l in enumerate(g["lanes"]):
+        np.testing.assert_array_equal(u_tw[j], l["u0_twin"])
+        np.testing.assert_array_equal(u_lit[j], l["u0_literal"])
+        np.testing.assert_allclose(u_q[j], l["u0_quad"], rtol=0, atol=1e-9)
+        dt, dl = np.abs(u_tw[j] - u_q[j]).max(), np.abs(u_lit[j] - u_q[j]).max()
+        side = "twin" if dt <= 1e-6 < dl else "literal" if dl <= 1e-6 < dt else "both" if max(dt, dl) <= 1e-6 else "neither"
+        assert side == l["side"], (l["lane"], side, l["side"])

@@ -192,14 +192,15 @@ def test_closed_loop_disturbance_matches_oracle(oracle):
                                        dist_amp=amp, xwidth=xw)
     ref, st = _stable_lanes(oracle, run, x0)
     assert st.mean() > 0.5, st.mean()
-    # the disturbed state itself (step td, before the solve): x, y, theta as the literal oracle to
-    # 1e-8 on the stable lanes (the first td - 1 closed-loop steps carry the two formulations'
-    # rounding differences; bit-for-bit equality with the kernel-order twin is
-    # tests/test_gpu_twin.py::test_closed_loop_bit_identical); the re-projected s to 1e-6 (a target
-    # near a circular arc's centre makes the minimiser flat: the formulations' Newton iterations stop
-    # a little apart -- measured up to 2.7e-6 since the explicit-FMA formulation, 1e-6 before)
-    np.testing.assert_allclose(r["X"][st, td - 1, :3], ref["X"][st, td - 1, :3], rtol=0, atol=1e-8)
-    np.testing.assert_allclose(r["X"][:, td - 1, 3], ref["X"][:, td - 1, 3], rtol=0, atol=1e-5)
+    # the disturbed state itself (step td, before the solve), re-projected s included, as the literal
+    # oracle to 1e-8 on the stable lanes (the first td - 1 closed-loop steps carry the two
+    # formulations' rounding differences; bit-for-bit equality with the kernel-order twin is
+    # tests/test_gpu_twin.py::test_closed_loop_variants_bit_identical).  Measured: <= 2.4e-10 on every
+    # stable lane; lane 0 is not one -- its closed loop is chaotic before the disturbance (its pre-disturbance state
+    # already differs by 3.4e-6 between the two formulations, so its re-projected s by 2.7e-6; the
+    # round-3 note blamed the Newton stop, but the re-projection adds nothing measurable)
+    assert not st[0]
+    np.testing.assert_allclose(r["X"][st, td - 1, :], ref["X"][st, td - 1, :], rtol=0, atol=1e-8)
     assert np.abs(r["U"] - ref["U"]).max(axis=(1, 2))[st].max() < 1e-6
     assert np.abs(r["X"] - ref["X"]).max(axis=(1, 2))[st].max() < 1e-8
     # the re-projected s is wrapped into [-b, b) (helper.m:233)

@@ -6,8 +6,10 @@ random start index per lane, four shapes mixed per lane, K = 50 SQP-RTI iteratio
 * lanes are independent: a shuffled batch gives every lane the same bits, and so does a small
   batch holding some of the same lanes (the layout at N = 50 is two stages per lane, and the
   packing moves instances between waves and groups);
-* u0 agrees with the oracle on the first lanes that the oracle itself reproduces (the probe
-  criterion of tests/test_gpu_config2.py; full-step SQP at N = 50 settles on fewer lanes)."""
+* u0 agrees with the literal oracle on the first 1 024 lanes wherever neither implementation moves
+  under the probe criterion of tests/test_gpu_config2.py (full-step SQP at N = 50 settles on fewer
+  lanes); where they disagree, tests/test_extended_oracle.py and bench's configs4.parity_literal
+  adjudicate in extended precision."""
 import numpy as np
 import pytest
 
@@ -50,17 +52,36 @@ def test_config4_full_batch(oracle):
     small.close()
     np.testing.assert_array_equal(us, u[pick])
 
-    nl = 64
+    # the literal restatement (oracle/qsp_oracle.c) on the first 1 024 lanes, with the probe criterion
+    # in both implementations: the oracle's own response to three 1e-13 relative x0 perturbations and
+    # mu_stop 1.5e-10, the GPU's to the same x0 perturbations
+    nl = 1024
 
     def run(xx, **kw):
         return oracle.controller_solve(make_opts(N=N, sqp_iters=K, **kw), xx, traj, idx[:nl],
                                        oracle.new_warm(nl, N), shape_id=sid[:nl])
     ref = run(x0[:nl])
-    dev = np.zeros(nl)
+    xdev = np.zeros(nl)
     for f in (1e-13, -1e-13, 3e-13):
-        dev = np.maximum(dev, np.abs(run(x0[:nl] * (1 + f))["u0"] - ref["u0"]).max(1))
-    dev = np.maximum(dev, np.abs(run(x0[:nl], mu_stop=1.5e-10)["u0"] - ref["u0"]).max(1))
+        xdev = np.maximum(xdev, np.abs(run(x0[:nl] * (1 + f))["u0"] - ref["u0"]).max(1))
+    dev = np.maximum(xdev, np.abs(run(x0[:nl], mu_stop=1.5e-10)["u0"] - ref["u0"]).max(1))
+    s = _solver(nl, N, K)
+    s.set_reference_trajectory(traj)
+    s.set_shape_ids(sid[:nl])
+    gdev = np.zeros(nl)
+    for f in (1e-13, -1e-13, 3e-13):
+        s.controller_reset()
+        gdev = np.maximum(gdev, np.abs(s.controller_solve(x0[:nl] * (1 + f), idx[:nl]) - u[:nl]).max(1))
+    s.close()
     nonchaotic = (dev < 1e-9) & (ref["status"] == 0)
     d = np.abs(u[:nl] - ref["u0"]).max(1)
-    assert nonchaotic.sum() >= 10, nonchaotic.sum()
-    assert np.mean(d[nonchaotic] < 1e-6) >= 0.95, np.sort(d[nonchaotic])[-5:]
+    # measured (twin = GPU bit for bit, 1 024 lanes): N = 50's full-step SQP settles on fewer lanes
+    # than N = 20 -- 37 % of them move by > 1e-6 under the 1e-13 x0 probes, in both implementations,
+    # 73 % of the oracle's once mu_stop moves too -- and on every lane that neither implementation's
+    # probes move, the two agree within 1e-6 (240 lanes at 1e-9, 278 at 1e-6, none off)
+    assert nonchaotic.sum() >= 200, nonchaotic.sum()
+    assert d[nonchaotic].max() < 1e-6, np.sort(d[nonchaotic])[-5:]
+    both = (dev <= 1e-6) & (gdev <= 1e-6)
+    assert both.sum() >= 250, both.sum()
+    assert np.all(d[both] <= 1e-6), np.flatnonzero(both & (d > 1e-6))[:10]
+    assert abs(np.mean(gdev > 1e-6) - np.mean(xdev > 1e-6)) < 0.05, (np.mean(gdev > 1e-6), np.mean(xdev > 1e-6))

@@ -345,3 +345,33 @@ def test_closed_loop_variants_bit_identical(twin, N, nlp, delay, plant_delay, t_
                          delay_cols=D, plant_delay_cols=Dp, dist_step=t_dist, dist_amp=amp, xwidth=xw)
     for k in ("X", "Xsim", "U", "status"):
         same(g[k], t[k], f"closed loop {k}")
+
+
+def test_closed_loops_back_to_back_keep_the_controller_buffer(twin):
+    """qsp_closed_loop_ex keeps the controller's input buffer u_buff_contr across calls (it belongs to
+    the controller object, NMPC_controller.m:109, and persists across helper.closed_loop_matlab runs);
+    only set_delay_comp zeroes it.  A second closed loop on the same handle therefore equals the twin's
+    closed loop started from the buffer the first one left (its last D inputs, newest first), bit for
+    bit -- and differs from a run with a zeroed buffer."""
+    from oracle.oracle import make_opts
+    N, B, T, K = 10, 128, 8, 3
+    x0 = config2_x0(B, 515)
+    traj = straight_traj()
+    sid = np.arange(B) % 4
+    s = solver(N, B, sqp_iters=K)
+    s.set_shape_ids(sid)
+    s.set_reference_trajectory(traj)
+    s.set_delay_comp(0.15)
+    D = s.delay_cols()
+    assert D == 3
+    g1 = s.closed_loop(x0, T)
+    g2 = s.closed_loop(x0, T)                     # same handle, no set_delay_comp in between
+    s.close()
+    op = make_opts(N=N, sqp_iters=K)
+    t1 = twin.closed_loop(op, x0, traj, T, shape_id=sid, delay_cols=D)
+    same(g1["U"], t1["U"], "first loop U")
+    ub = np.ascontiguousarray(g1["U"][:, ::-1][:, :D])   # u_buff_contr after the first loop: newest first
+    t2 = twin.closed_loop(op, x0, traj, T, shape_id=sid, delay_cols=D, ubc0=ub)
+    for k in ("X", "U", "status"):
+        same(g2[k], t2[k], f"second loop {k}")
+    assert np.abs(g2["U"] - g1["U"]).max() > 1e-6    # the carried buffer changed the second loop

@@ -44,3 +44,26 @@ def test_qp_solver_cond_N_checked_before_any_device_call():
     for bad in (0, 21, 2.5, -1):
         with pytest.raises(ValueError):
             OcpSolver(N=20, qp_solver_cond_N=bad)
+
+
+def test_controller_and_mex_option_mappings_agree():
+    """The two front-ends of the reference controller -- NMPCController (Python) and the MEX gateway
+    (integration/matlab/qsp_nmpc_mex.c) -- map nlp_solver_type to the same QP iteration cap: acados'
+    qp_solver_iter_max default 50 for 'SQP' (the reference's setting), the library's 20 for SQP_RTI;
+    and the same SQP iteration defaults (30 / 1 in the MEX, 30 in the mirror's ctor)."""
+    import os
+    import re
+    from uclv_qs_pushing_matlab_amd.controller import NMPCController
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "matlab",
+                            "qsp_nmpc_mex.c")).read()
+    m = re.search(r'"qp_solver_iter_max",\s*o\.nlp_mode == QSP_NLP_SQP_MERIT \? (\d+) : o\.qp_iters\)', src)
+    assert m, "MEX qp_solver_iter_max mapping not found"
+    mex_sqp_cap = int(m.group(1))
+    m2 = re.search(r'"nlp_solver_max_iter",\s*o\.nlp_mode == QSP_NLP_SQP_MERIT \? (\d+) : (\d+)\)', src)
+    assert m2
+    sqp = NMPCController("c", None, 0.05, 10, nlp_solver_type="SQP")
+    rti = NMPCController("c", None, 0.05, 10, nlp_solver_type="SQP_RTI")
+    assert sqp._opts["qp_iters"] == mex_sqp_cap == 50
+    assert rti._opts["qp_iters"] == 20      # the MEX keeps qsp_default_options' 20 for SQP_RTI
+    assert sqp._opts["sqp_iters"] == int(m2.group(1)) == 30
+    assert NMPCController("c", None, 0.05, 10, nlp_solver_type="SQP", qp_iters=7)._opts["qp_iters"] == 7

@@ -19,10 +19,15 @@ from .solver import OcpSolver
 
 
 class NMPCController:
-    def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=20,
+    def __init__(self, name, plant, sample_time, Hp, batch=1, nlp_solver_type="SQP", sqp_iters=30, qp_iters=None,
                  device=0, stages_per_lane=0, qp_solver_cond_N=5):
         # create_ocp_opts (:270-300): 'SQP' with merit backtracking, max_iter 30, tol 1e-6;
-        # nlp_solver_type='SQP_RTI' gives the fixed-K full-step iteration of the BASELINE metric
+        # nlp_solver_type='SQP_RTI' gives the fixed-K full-step iteration of the BASELINE metric.
+        # qp_iters: the QP iteration cap -- acados' qp_solver_iter_max default 50 (the reference leaves
+        # it) for 'SQP', as the MEX gateway sets it (integration/matlab/qsp_nmpc_mex.c); the library's
+        # 20 for the fixed-K 'SQP_RTI' metric
+        if qp_iters is None:
+            qp_iters = 50 if nlp_solver_type == "SQP" else 20
         self.name = name
         self.plant = plant
         self.sample_time = sample_time
