@@ -207,13 +207,22 @@ static void cmd_get(qsp_solver* h, mxArray* plhs[], int nrhs, const mxArray* prh
     char f[32];
     if (mxGetString(prhs[2], f, sizeof f)) mexErrMsgIdAndTxt("qsp:field", "get: field name");
     const int staged = nrhs > 3;
-    if (!strcmp(f, "status") || !strcmp(f, "sqp_iter") || !strcmp(f, "qp_iter") || !strcmp(f, "qp_capped")) {
+    if (!strcmp(f, "status") || !strcmp(f, "sqp_iter") || !strcmp(f, "qp_iter") || !strcmp(f, "qp_capped") ||
+        !strcmp(f, "qp_stalled")) {
         plhs[0] = mxCreateNumericMatrix(1, B, mxINT32_CLASS, mxREAL);
         int32_t* d = (int32_t*)mxGetData(plhs[0]);
         if (!strcmp(f, "status")) check(qsp_get_status(h, d), "qsp_get_status");
         else if (!strcmp(f, "sqp_iter")) check(qsp_get_sqp_iter(h, d), "qsp_get_sqp_iter");
         else if (!strcmp(f, "qp_iter")) check(qsp_get_qp_iter(h, d), "qsp_get_qp_iter");
+        else if (!strcmp(f, "qp_stalled")) check(qsp_get_qp_stalled(h, d), "qsp_get_qp_stalled");
         else check(qsp_get_qp_capped(h, d), "qsp_get_qp_capped");
+        return;
+    }
+    if (!strcmp(f, "residuals")) {
+        /* res_stat, res_eq, res_ineq, res_comp of each lane's last KKT test ('sqp' only): the
+         * residual columns of acados' get('stat') at the lane's last iteration; 4 x B */
+        plhs[0] = mxCreateDoubleMatrix(4, B, mxREAL);
+        check(qsp_get_residuals(h, mxGetPr(plhs[0])), "qsp_get_residuals");
         return;
     }
     if (!strcmp(f, "time_tot") || !strcmp(f, "time_lin") || !strcmp(f, "time_qp_sol")) {

@@ -89,6 +89,7 @@ int main(int argc, char** argv) {
     /* closed loop: u = solve(x, i); plant x += Ts f(x, u) (helper.m:292-307) */
     double U[STEPS][2], X[STEPS + 1][4] = {{0}};
     int32_t ST[STEPS], IT[STEPS];
+    double RES[STEPS][4];
     double tl = 0, tq = 0, tt = 0;
     for (int i = 0; i < STEPS; ++i) {
         mxArray* u = NULL;
@@ -100,6 +101,9 @@ int main(int argc, char** argv) {
         ST[i] = ((int32_t*)mxGetData(st))[0];
         CALL(1, &st, stub_string("get"), h, stub_string("sqp_iter"));
         IT[i] = ((int32_t*)mxGetData(st))[0];
+        mxArray* rs = NULL;
+        CALL(1, &rs, stub_string("get"), h, stub_string("residuals"));   /* 4 x 1 */
+        for (int c = 0; c < 4; ++c) RES[i][c] = mxGetPr(rs)[c];
         mxArray* tv = NULL;
         CALL(1, &tv, stub_string("get"), h, stub_string("time_lin"));
         tl += mxGetScalar(tv);
@@ -124,6 +128,7 @@ int main(int argc, char** argv) {
     fwrite(IT, sizeof IT, 1, fo);
     const double tail[4] = {(double)errors, tl, tq, tt};
     fwrite(tail, sizeof tail, 1, fo);
+    fwrite(RES, sizeof RES, 1, fo);
     fclose(fo);
     return 0;
 }

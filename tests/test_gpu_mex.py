@@ -37,6 +37,7 @@ def test_mex_gateway_drives_main_m(tmp_path):
     st = np.frombuffer(raw, np.int32, S, off)
     it = np.frombuffer(raw, np.int32, S, off + 4 * S)
     errors, t_lin, t_qp, t_tot = np.frombuffer(raw, np.float64, 4, off + 8 * S)
+    res = np.frombuffer(raw, np.float64, S * 4, off + 8 * S + 32).reshape(S, 4)
     assert errors == 7
     gold = np.load(os.path.join(GOLDEN, "main_m_sqp_closed_loop.npz"))
     np.testing.assert_allclose(U, gold["U"], rtol=0, atol=1e-7)
@@ -44,3 +45,8 @@ def test_mex_gateway_drives_main_m(tmp_path):
     np.testing.assert_array_equal(st, gold["status"])
     assert np.mean(it == gold["iters"]) > 0.95
     assert t_qp > 0 and t_lin > 0 and t_tot >= t_qp
+    # get('residuals'): the KKT residuals of each step's last test -- all below tol 1e-6 where the
+    # SQP converged, at least one at or above it where it stopped at max_iter
+    conv, capped = st == 0, st == 2
+    assert np.all(res[conv] < 1e-6)
+    assert np.all(res[capped].max(1) >= 1e-6)
