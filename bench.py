@@ -120,7 +120,14 @@ def host_cpu():
     except AttributeError:
         aff = os.cpu_count() or 1
     env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return dict(nproc=os.cpu_count(), affinity_cpus=aff, model=model, threads=max(1, env or aff))
+    quota = None   # the cgroup's CPU quota (cgroup v2 cpu.max "max 100000" = none), in CPUs
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return dict(nproc=os.cpu_count(), affinity_cpus=aff, model=model, threads=max(1, env or aff), cgroup_cpus=quota)
 
 
 def device_facts(dev):
@@ -815,7 +822,7 @@ def main():
                                         qp_iters=args.qp_iters)
         result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
                                   "host_nproc": hc["nproc"], "host_affinity_cpus": hc["affinity_cpus"],
-                                  "cpu_model": hc["model"],
+                                  "host_cgroup_cpu_quota": hc["cgroup_cpus"], "cpu_model": hc["model"],
                                   "sample": f"{n} lanes of the same workload (oracle/qsp_twin.c: the library's "
                                             f"formulation on the CPU, OpenMP over {threads} threads, {dt:.1f} s)"}
         result["cpu_baseline"]["thread_scaling"] = thread_scaling(run_t, n / dt, threads, hc["affinity_cpus"])
