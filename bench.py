@@ -851,6 +851,17 @@ def main():
         # formulations' differences (span-based de Boor + hand-derived Jacobian vs basis sum + AD)
         pl["twin_vs_literal_max_abs_u0_err"] = float(np.abs(rt_all["u0"][:nl] - rl["u0"]).max())
         result["parity_literal"] = pl
+        # the independent parity in one place beside the bit-exact one: agreement with the literal
+        # restatement, and how the disagreements that survive every probe are adjudicated in __float128
+        ep = pl.get("extended_precision", {})
+        sb = ep.get("stable_in_both", {})
+        result["parity"]["independent"] = {
+            "reference": "oracle/qsp_oracle.c (literal restatement), adjudicated by its __float128 build",
+            "lanes": pl["lanes"], "frac_within_1e-6": pl["frac_lanes_err_le_1e-6"],
+            "literal_self_frac_within_1e-6": pl["oracle_self_frac_le_1e-6"],
+            "disagreeing_stable_in_both": sb.get("lanes", 0),
+            "of_those_quad_sides_with_gpu": sb.get("sides_with_gpu", 0),
+            "of_those_quad_sides_with_literal": sb.get("sides_with_literal", 0)}
         if "configs1" in result:
             # configs[1] on the CPU in full (the twin: rate and bit-for-bit parity of every lane)
             x1, traj1, sid1 = config1_inputs(N)
