@@ -166,10 +166,12 @@ def flops_per_solve(N, K, qp_iter_total):
     return K * N * FLOP_LIN_STAGE + qp_iter_total * N * FLOP_IPM_STAGE
 
 
-def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20, idx=1):
+def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20, idx=1,
+                 sample=None):
     """The CPU restatement (port) timed on a bounded sample of the same workload (cold-start
     controller solves): the kernel-order twin (twin=True: the library's formulation on the CPU,
-    OpenMP over lanes) or the literal oracle.  idx: index_time (scalar, or per lane)."""
+    OpenMP over lanes) or the literal oracle.  idx: index_time (scalar, or per lane).  sample: a
+    fixed lane count instead of the target_s time budget (no probe run)."""
     from oracle.oracle import Oracle, make_opts
     orc = Oracle(SHAPES, twin=twin)
     op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=qp_iters)
@@ -186,12 +188,15 @@ def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=T
                                             precision=precision)
         return orc.controller_solve(o, xx, traj, idx_all[sl], warm, shape_id=shape_id[sl], nthreads=nt)
 
-    probe = min(len(x0), max(2 * threads, 16))
-    t0 = time.perf_counter()
-    run(slice(0, probe))
-    per = (time.perf_counter() - t0) / probe
-    n = int(min(len(x0), max(probe, target_s / max(per, 1e-7))))
-    n = min(len(x0), max(threads, (n // threads) * threads))
+    if sample is not None:
+        n = min(len(x0), int(sample))
+    else:
+        probe = min(len(x0), max(2 * threads, 16))
+        t0 = time.perf_counter()
+        run(slice(0, probe))
+        per = (time.perf_counter() - t0) / probe
+        n = int(min(len(x0), max(probe, target_s / max(per, 1e-7))))
+        n = min(len(x0), max(threads, (n // threads) * threads))
     t0 = time.perf_counter()
     r = run(slice(0, n))
     dt = time.perf_counter() - t0
@@ -885,8 +890,7 @@ def main():
             # precision adjudication of the disagreements (as parity_literal above)
             n4 = min(1024, len(x4))
             _, _, r4l, run4 = cpu_baseline(x4[:n4], traj4, sid4[:n4], 50, K, 0.0, threads, 0, twin=False,
-                                           qp_iters=args.qp_iters, idx=idx4b[:n4])
-            r4l = run4(slice(0, n4))
+                                           qp_iters=args.qp_iters, idx=idx4b[:n4], sample=n4)
             pl4 = parity_leg(u4_gpu[:n4], x4[:n4], traj4, sid4[:n4], 50, K, n4, r4l, run4, "SQP_RTI_N50",
                              gpu_dev4[:n4], qp_iters=args.qp_iters, ext_lanes=16)
             result["configs4"]["parity_literal"] = pl4
