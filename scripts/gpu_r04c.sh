@@ -6,6 +6,9 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 R=${R:-gpurun_out/r04c}
 mkdir -p $R
 export TMPDIR=/tmp
+timeout -k 10 120 ./scripts/ubench/riccati_scan_s2 50 16384 10 36 > $R/riccati_scan_s2.txt 2>&1 || { cat $R/riccati_scan_s2.txt; exit 1; }
+timeout -k 10 120 ./scripts/ubench/riccati_scan_s2 50 16384 10 0 >> $R/riccati_scan_s2.txt 2>&1 || { cat $R/riccati_scan_s2.txt; exit 1; }
+cat $R/riccati_scan_s2.txt
 OUT=$R/pmc_cfg4 ARGS="--config 4 --no-cpu --steps 1 --warmup 0" bash scripts/prof_pmc.sh || exit $?
 head -60 $R/pmc_cfg4/summary.txt
 timeout -k 10 600 python bench.py --closed-loop --steps 2 > $R/closed_loop.json 2> $R/closed_loop.err || { tail -20 $R/closed_loop.err; exit 1; }
