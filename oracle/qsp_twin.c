@@ -621,6 +621,139 @@ static void apply_step(tw_stage *s, double alpha)
     }
 }
 
+/* ---- S = 2: the affine passes as scans (qsp_solver.hip Aff, aff_*; riccati_solve<2, ...>) */
+typedef struct { double F[16], c[4]; } tw_aff;   /* x -> F x + c */
+
+/* g <- g o f, in place row by row (aff_compose) */
+static void aff_compose(tw_aff *g, const tw_aff *f)
+{
+    for (int i = 0; i < 4; ++i) {
+        double r[5];
+        for (int j = 0; j < 4; ++j)
+            r[j] = qfma(g->F[4 * i + 3], f->F[12 + j], qfma(g->F[4 * i + 2], f->F[8 + j],
+                        qfma(g->F[4 * i + 1], f->F[4 + j], g->F[4 * i] * f->F[j])));
+        r[4] = qfma(g->F[4 * i + 3], f->c[3], qfma(g->F[4 * i + 2], f->c[2], qfma(g->F[4 * i + 1], f->c[1],
+                    qfma(g->F[4 * i], f->c[0], g->c[i]))));
+        for (int j = 0; j < 4; ++j) g->F[4 * i + j] = r[j];
+        g->c[i] = r[4];
+    }
+}
+static void aff_apply(const tw_aff *m, const double x[4], double y[4])
+{
+    for (int i = 0; i < 4; ++i)
+        y[i] = qfma(m->F[4 * i + 3], x[3], qfma(m->F[4 * i + 2], x[2], qfma(m->F[4 * i + 1], x[1], qfma(m->F[4 * i], x[0], m->c[i]))));
+}
+static void aff_identity(tw_aff *m)
+{
+    for (int q = 0; q < 16; ++q) m->F[q] = (q % 5 == 0) ? 1.0 : 0.0;
+    for (int q = 0; q < 4; ++q) m->c[q] = 0.0;
+}
+static void aff_forward(const tw_stage *s, tw_aff *m)
+{
+    const double *a = s->a, *B = s->B, *K = s->K;
+    const double Am[4][4] = {{1.0, 0.0, a[0], a[1]}, {0.0, 1.0, a[2], a[3]}, {0.0, 0.0, 1.0, a[4]}, {0.0, 0.0, 0.0, a[5]}};
+    for (int i = 0; i < 4; ++i) {
+        for (int q = 0; q < 4; ++q) m->F[4 * i + q] = qfma(B[2 * i + 1], K[4 + q], qfma(B[2 * i], K[q], Am[i][q]));
+        m->c[i] = qfma(B[2 * i + 1], s->kk[1], qfma(B[2 * i], s->kk[0], s->bb[i]));
+    }
+}
+static void aff_delta(const tw_stage *s, double dgx3, const double dgu[2], tw_aff *m)
+{
+    const double *a = s->a, *B = s->B, *K = s->K;
+    const double Am[4][4] = {{1.0, 0.0, a[0], a[1]}, {0.0, 1.0, a[2], a[3]}, {0.0, 0.0, 1.0, a[4]}, {0.0, 0.0, 0.0, a[5]}};
+    for (int i = 0; i < 4; ++i) {
+        for (int q = 0; q < 4; ++q) m->F[4 * q + i] = qfma(B[2 * i + 1], K[4 + q], qfma(B[2 * i], K[q], Am[i][q]));
+        m->c[i] = qfma(K[4 + i], dgu[1], qfma(K[i], dgu[0], i == 3 ? dgx3 : 0.0));
+    }
+}
+
+/* the S = 2 difference pass: suffix scan of the lanes' backward maps (slot 1's, then slot 0's;
+ * identity past the horizon), dp_N = 0; each slot's dkk from the dp reaching it */
+static void delta_scan_s2(const tw_par *p, tw_stage *st, const double *gx3, double (*gu)[2])
+{
+    const int N = p->N, L = p->L;
+    tw_aff d[64], nd[64];
+    for (int l = 0; l < L; ++l) {
+        const int k0 = 2 * l;
+        if (k0 + 1 < N) {
+            tw_aff m1;
+            aff_delta(st + k0, gx3[k0], gu[k0], d + l);
+            aff_delta(st + k0 + 1, gx3[k0 + 1], gu[k0 + 1], &m1);
+            aff_compose(d + l, &m1);
+        } else if (k0 < N) {
+            aff_delta(st + k0, gx3[k0], gu[k0], d + l);
+        } else {
+            aff_identity(d + l);
+        }
+    }
+    for (int off = 1; off < L; off <<= 1) {
+        for (int l = 0; l < L; ++l) {
+            nd[l] = d[l];
+            if (l + off < L) aff_compose(nd + l, d + l + off);
+        }
+        memcpy(d, nd, sizeof(tw_aff) * (size_t)L);
+    }
+    for (int l = 0; l < L; ++l) {
+        double pv[4];
+        for (int i = 0; i < 4; ++i) pv[i] = (l + 1 < L) ? d[l + 1].c[i] : 0.0;
+        for (int ls = 1; ls >= 0; --ls) {
+            const int k = 2 * l + ls;
+            if (k < N) {
+                tw_stage *s = st + k;
+                double dkk[2];
+                ric_delta_step(s->a, s->B, gx3[k], gu[k], s->K, s->Rn, pv, dkk);
+                s->kk[0] += dkk[0];
+                s->kk[1] += dkk[1];
+            }
+        }
+    }
+}
+
+/* the S = 2 forward pass: prefix scan of the lanes' closed-loop maps (slot 0's, then slot 1's); the
+ * state entering lane l is T_{l-1}(dx0); slot 0 forms du and steps the dynamics, slot 1 forms du */
+static void forward_scan_s2(const tw_par *p, tw_stage *st, const double dx0[4], int factor)
+{
+    const int N = p->N, L = p->L;
+    tw_aff e[64], ne[64];
+    for (int l = 0; l < L; ++l) {
+        const int k0 = 2 * l;
+        if (k0 + 1 < N) {   /* the last lane's map is consumed by no lane (values there are unused) */
+            tw_aff m1;
+            aff_forward(st + k0, e + l);
+            aff_forward(st + k0 + 1, &m1);
+            aff_compose(&m1, e + l);
+            e[l] = m1;
+        } else {
+            aff_identity(e + l);
+        }
+    }
+    for (int off = 1; off < L; off <<= 1) {
+        for (int l = 0; l < L; ++l) {
+            ne[l] = e[l];
+            if (l >= off) aff_compose(ne + l, e + l - off);
+        }
+        memcpy(e, ne, sizeof(tw_aff) * (size_t)L);
+    }
+    for (int l = 0; l < L; ++l) {
+        double dx[4];
+        if (l == 0) memcpy(dx, dx0, sizeof dx);
+        else aff_apply(e + l - 1, dx0, dx);
+        for (int ls = 0; ls < 2; ++ls) {
+            const int k = 2 * l + ls;
+            if (k >= N) break;
+            tw_stage *s = st + k;
+            double du[2];
+            du[0] = qfma(s->K[3], dx[3], qfma(s->K[2], dx[2], qfma(s->K[1], dx[1], qfma(s->K[0], dx[0], s->kk[0]))));
+            du[1] = qfma(s->K[7], dx[3], qfma(s->K[6], dx[2], qfma(s->K[5], dx[1], qfma(s->K[4], dx[0], s->kk[1]))));
+            double *out = factor ? s->VA : s->VN;
+            out[0] = dx[3];
+            out[1] = du[0];
+            out[2] = du[1];
+            if (ls == 0) dyn_step(s->a, s->B, s->bb, du, dx);
+        }
+    }
+}
+
 /* riccati_solve: factor (predictor) or the corrector's difference recursion, then the forward pass
  * writing the bounded solution components into VA (factor) / VN (corrector) */
 static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], int factor)
@@ -662,6 +795,8 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
                 memcpy(dp, n, sizeof dp);
             }
         }
+    } else if (S == 2 && !factor) {
+        delta_scan_s2(p, st, gx3, gu);
     } else {
         if (factor) {
             for (int i = 0; i < 10; ++i) P[i] = 0.0;
@@ -709,6 +844,10 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
                 n[i] = qfma(s->M[4 * i + 3], dx[3], qfma(s->M[4 * i + 2], dx[2], qfma(s->M[4 * i + 1], dx[1], qfma(s->M[4 * i], dx[0], cv[i]))));
             memcpy(dx, n, sizeof dx);
         }
+        return;
+    }
+    if (S == 2) {
+        forward_scan_s2(p, st, dx0, factor);
         return;
     }
     for (int k = 0; k < N; ++k) {

@@ -372,6 +372,74 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
     dx[0] = n0; dx[1] = n1; dx[2] = n2; dx[3] = n3;
 }
 
+// ------------------------------------------------ S = 2: the affine passes as scans
+// With two stages per lane (N + 1 > 32: configs[4]) the kernel runs one wave per SIMD, where a
+// serial lane walk is latency-bound.  The forward passes and the corrector's difference pass are
+// affine recursions, so they run as Hillis-Steele scans over the group's lanes instead
+// (scripts/ubench/fwd_scan_s2.hip: 0.50x the walk's time at that occupancy).  Partner maps move by
+// ds_bpermute; every composition is a fixed FMA order, restated by the oracle's twin.
+struct Aff { double F[16], c[4]; };   // x -> F x + c
+
+__device__ __forceinline__ double lane_read(double v, int src) {
+    const int lo = __shfl(__double2loint(v), src), hi = __shfl(__double2hiint(v), src);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void aff_read(const Aff& e, int src, Aff& f) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) f.F[q] = lane_read(e.F[q], src);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f.c[q] = lane_read(e.c[q], src);
+}
+// g <- g o f (f applied first), in place row by row: row i of the result needs only row i of g
+__device__ __forceinline__ void aff_compose(Aff& g, const Aff& f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double r[5];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            r[j] = qfma(g.F[4 * i + 3], f.F[12 + j], qfma(g.F[4 * i + 2], f.F[8 + j],
+                        qfma(g.F[4 * i + 1], f.F[4 + j], g.F[4 * i] * f.F[j])));
+        r[4] = qfma(g.F[4 * i + 3], f.c[3], qfma(g.F[4 * i + 2], f.c[2], qfma(g.F[4 * i + 1], f.c[1],
+                    qfma(g.F[4 * i], f.c[0], g.c[i]))));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g.F[4 * i + j] = r[j];
+        g.c[i] = r[4];
+    }
+}
+__device__ __forceinline__ void aff_apply(const Aff& m, const double x[4], double y[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        y[i] = qfma(m.F[4 * i + 3], x[3], qfma(m.F[4 * i + 2], x[2], qfma(m.F[4 * i + 1], x[1], qfma(m.F[4 * i], x[0], m.c[i]))));
+}
+__device__ __forceinline__ void aff_identity(Aff& m) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) m.F[q] = (q % 5 == 0) ? 1.0 : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m.c[q] = 0.0;
+}
+// closed-loop forward map of a stage: dx -> (A + B K) dx + (B kk + b)
+__device__ __forceinline__ void aff_forward(const double a[6], const double B[8], const double bb[4], const double K[8],
+                                            const double kk[2], Aff& m) {
+    const double Am[4][4] = {{1.0, 0.0, a[0], a[1]}, {0.0, 1.0, a[2], a[3]}, {0.0, 0.0, 1.0, a[4]}, {0.0, 0.0, 0.0, a[5]}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m.F[4 * i + q] = qfma(B[2 * i + 1], K[4 + q], qfma(B[2 * i], K[q], Am[i][q]));
+        m.c[i] = qfma(B[2 * i + 1], kk[1], qfma(B[2 * i], kk[0], bb[i]));
+    }
+}
+// backward map of the corrector's difference recursion: dp -> (A + B K)' dp + (K' dgu + dgx3 e3)
+__device__ __forceinline__ void aff_delta(const double a[6], const double B[8], const double K[8], double dgx3,
+                                          const double dgu[2], Aff& m) {
+    const double Am[4][4] = {{1.0, 0.0, a[0], a[1]}, {0.0, 1.0, a[2], a[3]}, {0.0, 0.0, 1.0, a[4]}, {0.0, 0.0, 0.0, a[5]}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m.F[4 * q + i] = qfma(B[2 * i + 1], K[4 + q], qfma(B[2 * i], K[q], Am[i][q]));
+        m.c[i] = qfma(K[4 + i], dgu[1], qfma(K[i], dgu[0], i == 3 ? dgx3 : 0.0));
+    }
+}
+
 // ------------------------------------------------------------------ QP core
 // Barrier terms of slot ls into LDS (predictor): hg[0..2] Hessian additions, hg[3..5]
 // gradient additions.  The corrector changes only the gradient (corrector_terms).
@@ -576,6 +644,41 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             st.kk[0][0] = qfma(Rn[1], rt[1], qfma(Rn[0], rt[0], st.kk[0][0]));
             st.kk[0][1] = qfma(Rn[2], rt[1], qfma(Rn[1], rt[0], st.kk[0][1]));
         }
+    } else if constexpr (S == 2 && !FACTOR) {
+        // corrector difference pass as a suffix scan of the lanes' backward maps, dp_N = 0: lane j's
+        // map is slot 1's then slot 0's (identity past the horizon); U_j = D_j o D_{j+1} o ...
+        const int k0 = 2 * c.lig;
+        Aff d;
+        {
+            Aff m1;
+            aff_delta(st.a[0], st.B[0], st.K[0], gx3[0], gu[0], d);
+            aff_delta(st.a[1], st.B[1], st.K[1], gx3[1], gu[1], m1);
+            if (k0 + 1 < c.N) aff_compose(d, m1);
+            else if (!(k0 < c.N)) aff_identity(d);
+        }
+        for (int off = 1; off < c.L; off <<= 1) {
+            const bool take = c.lig + off < c.L;
+            Aff f;
+            aff_read(d, take ? c.lane + off : c.lane, f);
+            if (take) aff_compose(d, f);
+        }
+        // dp_{2j+2}: the next lane's suffix map applied to dp_N = 0 (its constant); then each slot's
+        // dkk from the dp reaching it, slot 1 first (ric_delta_step also steps dp to the slot)
+        double pvs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const double nx = wave_from_next(d.c[i]);
+            pvs[i] = (c.lig + 1 < c.L) ? nx : 0.0;
+        }
+#pragma unroll
+        for (int ls = 1; ls >= 0; --ls) {
+            if (kof<S>(c, ls) < c.N) {
+                double dkk[2];
+                ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvs, dkk);
+                st.kk[ls][0] += dkk[0];
+                st.kk[ls][1] += dkk[1];
+            }
+        }
     } else
     for (int j = c.L - 1; j >= 0; --j) {
         // Lanes above j already hold their final factors and sit the step out (exec
@@ -658,6 +761,48 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             st.f(out, 0, 0) = dxk[3];
             st.f(out, 0, 1) = qfma(K[3], dxk[3], qfma(K[2], dxk[2], qfma(K[1], dxk[1], qfma(K[0], dxk[0], st.kk[0][0]))));
             st.f(out, 0, 2) = qfma(K[7], dxk[3], qfma(K[6], dxk[2], qfma(K[5], dxk[1], qfma(K[4], dxk[0], st.kk[0][1]))));
+        }
+        return;
+    }
+    if constexpr (S == 2) {
+        // forward pass as a prefix scan of the lanes' closed-loop maps (slot 0's, then slot 1's):
+        // T_j = E_j o T_{j-1}; the state entering lane j is T_{j-1}(dx0) (dx0 at lane 0), then
+        // slot 0 forms du = kk + K dx and steps the dynamics, slot 1 forms its du
+        Aff e;
+        {
+            Aff m1;
+            aff_forward(st.a[0], st.B[0], st.bb[0], st.K[0], st.kk[0], e);
+            aff_forward(st.a[1], st.B[1], st.bb[1], st.K[1], st.kk[1], m1);
+            aff_compose(m1, e);
+            e = m1;
+        }
+        for (int off = 1; off < c.L; off <<= 1) {
+            const bool take = c.lig >= off;
+            Aff f;
+            aff_read(e, take ? c.lane - off : c.lane, f);
+            if (take) aff_compose(e, f);
+        }
+        double dx[4];
+        {
+            double y[4];
+            aff_apply(e, dx0, y);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double pr = wave_from_prev(y[i]);
+                dx[i] = c.lig == 0 ? dx0[i] : pr;
+            }
+        }
+#pragma unroll
+        for (int ls = 0; ls < 2; ++ls) {
+            double du[2];
+            du[0] = qfma(st.K[ls][3], dx[3], qfma(st.K[ls][2], dx[2], qfma(st.K[ls][1], dx[1], qfma(st.K[ls][0], dx[0], st.kk[ls][0]))));
+            du[1] = qfma(st.K[ls][7], dx[3], qfma(st.K[ls][6], dx[2], qfma(st.K[ls][5], dx[1], qfma(st.K[ls][4], dx[0], st.kk[ls][1]))));
+            if (kof<S>(c, ls) < c.N) {
+                st.f(out, ls, 0) = dx[3];
+                st.f(out, ls, 1) = du[0];
+                st.f(out, ls, 2) = du[1];
+            }
+            if (ls == 0) dyn_step(st.a[0], st.B[0], st.bb[0], du, dx);
         }
         return;
     }
