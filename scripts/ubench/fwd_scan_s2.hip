@@ -179,6 +179,57 @@ __global__ void __launch_bounds__(64) scan_kernel(const double* in, const double
         }
 }
 
+
+// closed-loop walk on the lanes' composite maps (E = m1 o m0 per lane, built as the scan builds it):
+// dx entering lane j+1 = E_j dx entering lane j, one 4x4 affine step per lane under the lane mask
+__global__ void __launch_bounds__(64) cwalk_kernel(const double* in, const double* x0, double* out, int N, int nI,
+                                                   int reps) {
+    extern __shared__ double pad[];
+    const int lane = threadIdx.x & 63, L = (N + 2) / 2, G = 64 / L;
+    const int grp = lane / L, lig = lane - grp * L;
+    const int inst = blockIdx.x * G + grp;
+    const bool real = grp < G && inst < nI;
+    St s[2];
+#pragma unroll
+    for (int ls = 0; ls < 2; ++ls) {
+        const int k = 2 * lig + ls;
+        load(in + ((size_t)(real ? inst : 0) * N + (k < N ? k : N - 1)) * NIN, s[ls]);
+    }
+    if (threadIdx.x == 1000) pad[0] = 0.0;
+    double o[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    for (int r = 0; r < reps; ++r) {
+        Aff m0, e;
+        make_aff(s[0], m0);
+        make_aff(s[1], e);
+        compose(e, m0);
+        double dx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dx[q] = x0[(size_t)(real ? inst : 0) * 4 + q] + 1e-300 * o[0][0];
+        for (int j = 0; j < L - 1; ++j) {
+            if (lig >= j && lig < L - 1) {
+                double n[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) n[i] = fma(e.F[4 * i + 3], dx[3], fma(e.F[4 * i + 2], dx[2], fma(e.F[4 * i + 1], dx[1], fma(e.F[4 * i], dx[0], e.c[i]))));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dx[i] = from_prev(dx[i], n[i]);
+            }
+        }
+#pragma unroll
+        for (int ls = 0; ls < 2; ++ls) {
+            double du[2];
+            control(s[ls], dx, du);
+            o[ls][0] = dx[3]; o[ls][1] = du[0]; o[ls][2] = du[1];
+            if (ls == 0) dyn_step(s[0], du, dx);
+        }
+    }
+    if (real)
+        for (int ls = 0; ls < 2; ++ls) {
+            const int k = 2 * lig + ls;
+            if (k < N)
+                for (int q = 0; q < 3; ++q) out[((size_t)inst * N + k) * 3 + q] = o[ls][q];
+        }
+}
+
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 50;
     const int nI = argc > 2 ? atoi(argv[2]) : 16384;
@@ -211,6 +262,10 @@ int main(int argc, char** argv) {
     const size_t lds = (size_t)ldsKB * 1024;
     CK(hipFuncSetAttribute((const void*)walk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     CK(hipFuncSetAttribute((const void*)scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void*)cwalk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    double* dc;
+    CK(hipMalloc(&dc, nout * 8));
+    float tc = 0;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -226,6 +281,11 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ts, e0, e1));
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(cwalk_kernel, dim3(blocks), dim3(64), lds, 0, din, dx0, dc, N, nI, reps);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&tc, e0, e1));
     }
     CK(hipGetLastError());
     std::vector<double> ow(nout), os(nout);
@@ -234,7 +294,12 @@ int main(int argc, char** argv) {
     double maxrel = 0.0, scale = 0.0;
     for (size_t q = 0; q < nout; ++q) scale = fmax(scale, fabs(ow[q]));
     for (size_t q = 0; q < nout; ++q) maxrel = fmax(maxrel, fabs(ow[q] - os[q]) / (scale + 1e-300));
-    printf("S=2 forward walk N=%d L=%d instances=%d reps=%d lds=%dKB: walk %.3f ms, scan %.3f ms (scan/walk %.2f); "
-           "max |walk - scan| / max|walk| = %.2e\n", N, L, nI, reps, ldsKB, tw / reps, ts / reps, ts / tw, maxrel);
+    std::vector<double> oc(nout);
+    CK(hipMemcpy(oc.data(), dc, nout * 8, hipMemcpyDeviceToHost));
+    double maxc = 0.0;
+    for (size_t q = 0; q < nout; ++q) maxc = fmax(maxc, fabs(ow[q] - oc[q]) / (scale + 1e-300));
+    printf("S=2 forward walk N=%d L=%d instances=%d reps=%d lds=%dKB: walk %.3f ms, scan %.3f ms (scan/walk %.2f), "
+           "closed-loop lane walk %.3f ms (%.2f); max |walk - scan| / max|walk| = %.2e, closed-loop %.2e\n", N, L, nI, reps,
+           ldsKB, tw / reps, ts / reps, ts / tw, tc / reps, tc / tw, maxrel, maxc);
     return 0;
 }
