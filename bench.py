@@ -559,7 +559,10 @@ def main():
     ndev = torch.cuda.device_count()
     gpu = local_rank % ndev if backend == "gloo" and ndev else local_rank
     dist = None
-    if world > 1:
+    # QSP_DIST_FORCE=1 opens the process group at world size 1 too (under torch.distributed.run): the
+    # one-GPU box can then run the RCCL branch (device tensors, barrier, MAX all_reduce, gather_lanes),
+    # since RCCL refuses two ranks on one device (tests/test_gpu_multirank.py)
+    if world > 1 or (os.environ.get("QSP_DIST_FORCE") == "1" and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         dist.init_process_group(backend)

@@ -39,3 +39,39 @@ def test_two_rank_bench_gather_matches_single_process(tmp_path):
     assert a["u0"].shape == (total, 2)
     np.testing.assert_array_equal(a["u0"], b["u0"])
     np.testing.assert_array_equal(a["status"], b["status"])
+
+
+def test_rccl_branch_world1_matches_single_process(tmp_path):
+    """The nccl (RCCL) branch of bench.py as the 8-GPU node runs it — process group on the nccl
+    backend, barriers and the MAX all_reduce on device tensors, gather_lanes on device u0/status —
+    executed on the box's one GPU at world size 1 (RCCL refuses two ranks on one device), started by
+    torch.distributed.run.  The gathered u0/status must equal a plain single-process run bit for bit."""
+    import json
+    import socket
+    total = 6144
+    common = ["--global-batch", str(total), "--steps", "1", "--warmup", "0", "--no-cpu", "--no-configs1",
+              "--no-configs4", "--no-closed-loop"]
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, QSP_DIST_FORCE="1", MASTER_ADDR="127.0.0.1")
+    env.pop("QSP_DIST_BACKEND", None)
+    env.pop("WORLD_SIZE", None)
+    rc = tmp_path / "rccl.npz"
+    one = tmp_path / "one.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--dump-u0", str(rc)] + common
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1 and rec["gather_ms"] is not None   # the gather ran (over RCCL)
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-u0", str(one)] + common,
+                        cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=200)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    assert json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][-1])["gather_ms"] is None
+    a, b = np.load(rc), np.load(one)
+    np.testing.assert_array_equal(a["u0"], b["u0"])
+    np.testing.assert_array_equal(a["status"], b["status"])
