@@ -173,6 +173,27 @@ def test_layouts_differ_by_rounding_only(twin):
     np.testing.assert_allclose(u[0], u[1], rtol=0, atol=1e-12)
 
 
+def test_s2_scans_across_horizons(twin):
+    """The S = 2 layout's scans (forward and corrector-difference passes as Hillis-Steele scans over
+    the group's lanes, at any lane count L = ceil((N+1)/2), powers of two or not) against the S = 1
+    lane walks for N = 2 ... 63, and against the literal restatement for N = 64 ... 127, where S = 1
+    no longer fits a wavefront: one SQP iteration, 64 lanes, mixed shapes.  Measured: <= 1e-17."""
+    nb = 64
+    x0 = config2_x0(nb, 11)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    for N in (2, 3, 5, 8, 11, 16, 17, 31, 32, 33, 47, 50, 63):
+        u = [twin.controller_solve(make_opts(N=N, sqp_iters=1, stages_per_lane=S), x0, traj, 1, twin.new_warm(nb, N),
+                                   shape_id=sid)["u0"] for S in (1, 2)]
+        np.testing.assert_allclose(u[1], u[0], rtol=0, atol=1e-15, err_msg=f"N={N}")
+    lit = Oracle(NAMES)
+    for N in (64, 100, 127):
+        r = twin.controller_solve(make_opts(N=N, sqp_iters=1, stages_per_lane=2), x0, traj, 1, twin.new_warm(nb, N),
+                                  shape_id=sid)
+        q = lit.controller_solve(make_opts(N=N, sqp_iters=1), x0, traj, 1, lit.new_warm(nb, N), shape_id=sid)
+        np.testing.assert_allclose(r["u0"], q["u0"], rtol=0, atol=1e-15, err_msg=f"N={N}")
+
+
 def test_divergence_exit(twin):
     """qp_mu_max below mu0 = 1: the first QP of every lane diverges by definition -> status 4
     (acados ACADOS_QP_FAILURE), sqp_iter 0, and the SQP keeps its initial iterate (u0 = the
