@@ -140,3 +140,12 @@ def test_mex_gateway_compiles(tmp_path):
                            os.path.join(ROOT, "tests", "stubs", "mex_stub.c"),
                            os.path.join(ROOT, "tests", "stubs", "mex_driver.c"),
                            "-L", lib, "-lqsp_nmpc", "-lm", "-o", str(tmp_path / "mex_driver")])
+
+
+def test_build_stamp_tracks_flags(monkeypatch):
+    """The in-tree library is current only while its digest stamp equals source_digest(), which
+    covers the compile flags: a flag change alone (e.g. a register-allocation option) rebuilds."""
+    from uclv_qs_pushing_matlab_amd import build as hb
+    assert not hb._stale()                                   # the library this checkout built
+    monkeypatch.setattr(hb, "FLAGS", hb.FLAGS + ["-DQSP_NOT_A_REAL_FLAG"])
+    assert hb._stale()
