@@ -146,6 +146,7 @@ def test_build_stamp_tracks_flags(monkeypatch):
     """The in-tree library is current only while its digest stamp equals source_digest(), which
     covers the compile flags: a flag change alone (e.g. a register-allocation option) rebuilds."""
     from uclv_qs_pushing_matlab_amd import build as hb
-    assert not hb._stale()                                   # the library this checkout built
+    hb.build()                                               # no-op when the library is current
+    assert not hb._stale()
     monkeypatch.setattr(hb, "FLAGS", hb.FLAGS + ["-DQSP_NOT_A_REAL_FLAG"])
     assert hb._stale()
