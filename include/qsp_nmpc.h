@@ -182,7 +182,11 @@ int qsp_get_qp_stalled(qsp_solver* s, int32_t* stalled /* B */);
 /* nlp_mode 1 only (else QSP_ERR_STATE): the NLP's KKT residuals of the last test each instance
  * evaluated -- acados' statistics res_stat, res_eq, res_ineq, res_comp (max norms; ocp_nlp_res of
  * the SQP with nlp_solver_tol_* at NMPC_controller.m:275-276).  For status 0 that is the test that
- * passed; for status 2 the test before the last QP; zeros for an instance that never iterated. */
+ * passed; for status 2 the test before the last QP (the final iterate after the max_iter-th step is
+ * not re-tested); zeros for an instance that never iterated, and before the first solve.
+ * Parity unpinned: the reference was run with acados v0.2.1; later acados releases re-linearise and
+ * test the final iterate at max_iter, which moves both these residuals and the status 0/2 boundary
+ * for an instance that converges on its last step.  No reference fixture fixes either behaviour. */
 int qsp_get_residuals(qsp_solver* s, double* res /* B x 4 */);
 int qsp_get_time_tot(qsp_solver* s, double* ms);                                        /* 'time_tot' */
 /* dims of the handle (outputs of a MEX/FFI layer are sized from these, never from caller input) */

@@ -10,7 +10,7 @@
  *   h = qsp_nmpc_mex('create', N, B, Ts [, opts])      % opts: struct, fields as acados_ocp_opts
  *        nlp_solver_type 'SQP' (default, + merit_backtracking) | 'SQP_RTI' (fixed K full steps)
  *        nlp_solver_max_iter (30 for SQP, 1 for SQP_RTI), nlp_solver_tol_stat/eq/ineq/comp (1e-6),
- *        qp_solver_iter_max (20), globalization_alpha_min (0.05), globalization_alpha_reduction
+ *        qp_solver_iter_max (50 for SQP, 20 for SQP_RTI), globalization_alpha_min (0.05), globalization_alpha_reduction
  *        (0.7), eps_sufficient_descent (1e-4), stage0_s_bound (1), stages_per_lane (0 = auto),
  *        device (0), qp_solver_cond_N (1..N; validated only, see below)  -- NMPC_controller.m:270-300
  *   d = qsp_nmpc_mex('dims', h)                          % [N B]
@@ -22,7 +22,8 @@
  *   qsp_nmpc_mex('ctrl_params', h, v_alpha, d_v, t_angle0, u_n_lb, u_t_ub)
  *   qsp_nmpc_mex('solve', h)                             % acados .solve()
  *   v = qsp_nmpc_mex('get', h, field [, stage])          % u (stage 0: 2 x B) | x | pi | cost |
- *        status | sqp_iter | qp_iter | qp_capped | time_tot | time_lin | time_qp_sol   (helper.m:253,264-269)
+ *        status | sqp_iter | qp_iter | qp_capped | qp_stalled | time_tot | time_lin | time_qp_sol
+ *        | residuals (4 x B: res_stat/eq/ineq/comp of the last KKT test, SQP only)   (helper.m:253,264-269)
  *   qsp_nmpc_mex('reference', h, y_ref)                  % 6 x T, set_reference_trajectory (:425-431)
  *   u0 = qsp_nmpc_mex('controller_solve', h, x0, index_time)   % NMPC_controller.solve (:329-423)
  *   qsp_nmpc_mex('delay_comp', h, delay)                 % set_delay_comp (:106-110)

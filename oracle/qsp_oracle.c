@@ -175,8 +175,9 @@ static real mat_mod(real a, real b)
 
 /* ================================================================ dynamics */
 /* f(x,u) and J = d f / d(x,u) (4 x 6, row-major) — PusherSliderModel.m:503-603 */
-/* motion-cone modes of the dynamics evaluations since the last reset, base 4 (diagnostics only) */
-static __thread int g_mode_code = 0;
+/* motion-cone modes of the dynamics evaluations since the last reset, base 4 (diagnostics only;
+ * unsigned: evaluations outside the SQP's reset points keep shifting it, which wraps, never UB) */
+static __thread uint32_t g_mode_code = 0;
 
 static void dynamics(const or_shape *sh, const real x[4], const real u[2], real f[4], real *J)
 {
@@ -249,7 +250,7 @@ static void dynamics(const or_shape *sh, const real x[4], const real u[2], real 
     /* indicator blend (:587-589); comparisons with NaN are false */
     dual ist = dmul(dind(rho.v >= gr.v), dind(rho.v <= gl.v));
     dual isl = dind(rho.v > gl.v), isr = dind(rho.v < gr.v);
-    g_mode_code = g_mode_code * 4 + (ist.v != 0.0 ? 0 : (isl.v != 0.0 ? 1 : (isr.v != 0.0 ? 2 : 3)));
+    g_mode_code = g_mode_code * 4u + (uint32_t)(ist.v != 0.0 ? 0 : (isl.v != 0.0 ? 1 : (isr.v != 0.0 ? 2 : 3)));
     for (int r = 0; r < 4; ++r) {
         dual v = dadd(dadd(dmul(ist, st[r]), dmul(isl, sl[r])), dmul(isr, sr[r]));
         f[r] = v.v;
@@ -664,7 +665,7 @@ typedef struct {
     int qp_total;
     int qp_capped;   /* QPs of this solve stopped by the iteration cap */
     int qp_stalled;  /* ... by the stall exit */
-    int mode[OR_MAX_N];  /* motion-cone modes of the stages' RK4 evaluations (diagnostics) */
+    uint32_t mode[OR_MAX_N];  /* motion-cone modes of the stages' RK4 evaluations (diagnostics) */
     real kkt[18];  /* diagnostics of the last NLP KKT test (nlp_mode 1): see or_set_kkt_diag */
 } or_ws;
 

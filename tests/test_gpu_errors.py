@@ -30,6 +30,21 @@ def test_state_and_argument_errors():
         s.set_shapes([bad])
     L = _lib.lib()
     assert L.qsp_set_reference_trajectory(s.handle, None, 10) == -1
+    with pytest.raises(_lib.QspError, match="nlp_mode 1"):
+        s.get("residuals")
+    s.close()
+    # residuals before the first solve: zeros (qsp_nmpc.h), not uninitialised device memory
+    for poison in ("0", "1"):
+        import os
+        os.environ["QSP_DEBUG_POISON"] = poison
+        try:
+            m = OcpSolver(N=10, batch=5, nlp_solver_type="SQP")
+        finally:
+            os.environ.pop("QSP_DEBUG_POISON")
+        np.testing.assert_array_equal(m.get("residuals"), np.zeros((5, 4)))
+        m.close()
+    s = OcpSolver(N=10, batch=4)
+    s.set_shapes([make_shape("santal")])
     with pytest.raises(ValueError):
         s.set("cost_y_ref", np.zeros((3, 3)))
     with pytest.raises(KeyError):

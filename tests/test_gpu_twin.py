@@ -102,29 +102,35 @@ def controller_pair(twin, N, B, x0, traj, sid, idx, K=50, steps=1, **kw):
     diag = np.zeros((B, 8))
     if nlp:
         twin.L.tw_set_kkt_diag(diag.ctypes.data_as(C.c_void_p))
-    s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI", **kw)
-    s.set_shape_ids(sid)
-    s.set_reference_trajectory(traj)
-    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp, qp_iters=kw.get("qp_iters", 20), qp_mu_max=kw.get("qp_mu_max", 1e100),
-                   stages_per_lane=kw.get("stages_per_lane", 0))
-    warm = twin.new_warm(B, N)
-    for step in range(steps):
-        u = s.controller_solve(x0, idx + step)
-        r = twin.controller_solve(op, x0, traj, idx + step, warm, shape_id=sid)
-        same(u, r["u0"], f"u0 (step {step})")
-        for f in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
-            same(s.get(f), r[{"sqp_iter": "iters"}.get(f, f)], f"{f} (step {step})")
-        same(s.get("x"), warm["X"], f"warm X (step {step})")
-        same(s.get("u"), warm["U"], f"warm U (step {step})")
-        same(s.get("pi"), warm["PI"], f"warm PI (step {step})")
-        same(s.get_cost(), r["cost"], f"cost (step {step})")
-        if nlp:   # the twin records the stationarity residual by block (u, x, terminal): the device its max
-            want = np.stack([diag[:, :3].max(1), diag[:, 3], diag[:, 4], diag[:, 5]], 1)
-            same(s.get("residuals"), want, f"KKT residuals (step {step})")
-            r["kkt"] = diag.copy()
-    if nlp:
-        twin.L.tw_set_kkt_diag(None)
-    s.close()
+    s = None
+    try:
+        s = solver(N, B, sqp_iters=K, nlp_solver_type="SQP" if nlp else "SQP_RTI", **kw)
+        s.set_shape_ids(sid)
+        s.set_reference_trajectory(traj)
+        op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp, qp_iters=kw.get("qp_iters", 20), qp_mu_max=kw.get("qp_mu_max", 1e100),
+                       stages_per_lane=kw.get("stages_per_lane", 0))
+        warm = twin.new_warm(B, N)
+        for step in range(steps):
+            u = s.controller_solve(x0, idx + step)
+            r = twin.controller_solve(op, x0, traj, idx + step, warm, shape_id=sid)
+            same(u, r["u0"], f"u0 (step {step})")
+            for f in ("status", "sqp_iter", "qp_iter", "qp_capped", "qp_stalled"):
+                same(s.get(f), r[{"sqp_iter": "iters"}.get(f, f)], f"{f} (step {step})")
+            same(s.get("x"), warm["X"], f"warm X (step {step})")
+            same(s.get("u"), warm["U"], f"warm U (step {step})")
+            same(s.get("pi"), warm["PI"], f"warm PI (step {step})")
+            same(s.get_cost(), r["cost"], f"cost (step {step})")
+            if nlp:   # the twin records the stationarity residual by block (u, x, terminal): the device its max
+                want = np.stack([diag[:, :3].max(1), diag[:, 3], diag[:, 4], diag[:, 5]], 1)
+                same(s.get("residuals"), want, f"KKT residuals (step {step})")
+                r["kkt"] = diag.copy()
+    finally:
+        # the twin writes through this process-global pointer on every later call: clear it on
+        # every exit path, a failed assertion included
+        if nlp:
+            twin.L.tw_set_kkt_diag(None)
+        if s is not None:
+            s.close()
     return r
 
 

@@ -24,12 +24,15 @@ def run(impl, B, K, steps, qp_iters, tol, **kw):
     op = make_opts(N=20, sqp_iters=K, nlp_mode=1, qp_iters=qp_iters, tol=tol, **kw)
     warm = orc.new_warm(B, 20)
     diag = np.zeros((B, 18 if impl == 'literal' else 8))
-    getattr(orc.L, ("tw_" if impl == "twin" else "or_") + "set_kkt_diag")(diag.ctypes.data_as(C.c_void_p))
+    setter = getattr(orc.L, ("tw_" if impl == "twin" else "or_") + "set_kkt_diag")
+    setter(diag.ctypes.data_as(C.c_void_p))
     out = []
-    for step in range(steps):
-        r = orc.controller_solve(op, x0, traj, 1 + step, warm, shape_id=sid)
-        out.append((r, diag.copy()))
-    getattr(orc.L, ("tw_" if impl == "twin" else "or_") + "set_kkt_diag")(None)
+    try:
+        for step in range(steps):
+            r = orc.controller_solve(op, x0, traj, 1 + step, warm, shape_id=sid)
+            out.append((r, diag.copy()))
+    finally:
+        setter(None)   # process-global pointer: never leave it set past this buffer's lifetime
     return out, sid
 
 
@@ -93,8 +96,10 @@ def closed_loop_breakdown(B=256, seed=None, qp_iters=50):
     op = make_opts(N=10, sqp_iters=30, nlp_mode=1, qp_iters=qp_iters)
     diag = np.zeros((B, 8))
     tw.L.tw_set_kkt_diag(diag.ctypes.data_as(C.c_void_p))
-    r = tw.closed_loop(op, x0, straight_traj(), 201, shape_id=sid, dist_step=300)
-    tw.L.tw_set_kkt_diag(None)
+    try:
+        r = tw.closed_loop(op, x0, straight_traj(), 201, shape_id=sid, dist_step=300)
+    finally:
+        tw.L.tw_set_kkt_diag(None)
     n2 = diag[:, 4].sum()
     st = r["status"]
     return {"lane_steps": int(st.size), "status": {int(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},

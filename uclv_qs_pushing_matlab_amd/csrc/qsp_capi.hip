@@ -438,7 +438,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     const char* pz = std::getenv("QSP_DEBUG_POISON");
     s->poison = pz && pz[0] == '1';
     if (s->poison) {
-        DevBuf* ws[] = {&s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wqp, &s->wperm, &s->wnit,
+        DevBuf* ws[] = {&s->wX, &s->wU, &s->wx0, &s->wlin, &s->wnlp, &s->wdone, &s->wres, &s->wqp, &s->wperm, &s->wnit,
                         &s->X, &s->U, &s->PI, &s->Xo, &s->Uo, &s->PIo, &s->u0, &s->cost, &s->yref, &s->yref_e};
         for (DevBuf* b : ws)
             if (e == hipSuccess && b->p) e = hipMemsetAsync(b->p, 0xff, b->n, s->stream);
@@ -447,6 +447,8 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
         if (e == hipSuccess) e = hipMemsetAsync(s->U.p, 0, B * N * 2 * 8, s->stream);
         if (e == hipSuccess) e = hipMemsetAsync(s->PI.p, 0, B * N * 4 * 8, s->stream);
     }
+    // qsp_get_residuals before the first solve returns zeros (header contract)
+    if (e == hipSuccess && s->wres.p) e = hipMemsetAsync(s->wres.p, 0, B * 4 * 8, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
         std::string m = std::string("qsp_create: ") + hipGetErrorString(e);

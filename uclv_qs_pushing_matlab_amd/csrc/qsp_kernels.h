@@ -47,7 +47,9 @@ struct SolveArgs {
     double* wnlp;              // 20 x B(N+1)     nlp_mode 1: PI(4), LAM(6), merit weights NU(4), ETA(6), SoA
     int32_t* wdone;            // B               nlp_mode 1: converged (KKT tolerances met)
     double* wres;              // B x 4           nlp_mode 1: the last KKT test's residuals (stat, eq, ineq, comp;
-                               //                 nullptr: not recorded)
+                               //                 nullptr: not recorded).  At max_iter (status 2) that is the test
+                               //                 before the last QP: the final iterate is not re-tested (acados
+                               //                 v0.2.1 semantics as restated; unpinned, qsp_nmpc.h)
     double* wqp;               // 16 x B(N+1)     nlp_mode 1: QP step dx(4), du(2), multipliers pi(4), lam(6), SoA
     int32_t* wperm;            // B               wave packing order of the QP kernel (nullptr: identity)
     int32_t* wnit;             // B               IPM iterations of each instance's last four QPs (8 bits each, last lowest)
