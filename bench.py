@@ -250,10 +250,20 @@ def extended_adjudication(u_gpu, u_lit, run, lanes_sets, max_lanes=64, control=N
     dt = np.abs(u_gpu[lanes] - uq).max(1)
     dl = np.abs(u_lit[lanes] - uq).max(1)
     ext_ok = np.abs(ul - uq).max(1) <= 1e-6
+    n_sel = len(names)
+    sel = np.arange(len(lanes)) < n_sel
     side = np.where((dt <= 1e-6) & (dl > 1e-6), "gpu", np.where((dl <= 1e-6) & (dt > 1e-6), "literal",
                     np.where((dt <= 1e-6) & (dl <= 1e-6), "both", "neither")))
     out = {"reference": "oracle/qsp_oracle.c in __float128 (libquadmath) and long double, the same formulas",
            "seconds": time.perf_counter() - t0}
+    # the metric against exact arithmetic where it has an answer: every adjudicated lane (disagreeing
+    # and control) on which long double and quad agree to 1e-6
+    if ext_ok.any():
+        out["extended_stable"] = {"lanes": int(ext_ok.sum()), "of_disagreeing": int(np.sum(ext_ok & sel)),
+                                  "max_abs_u0_err_gpu_vs_quad": float(dt[ext_ok].max()),
+                                  "max_abs_u0_err_literal_vs_quad": float(dl[ext_ok].max()),
+                                  "gpu_within_1e-6_of_quad": int(np.sum(ext_ok & (dt <= 1e-6))),
+                                  "literal_within_1e-6_of_quad": int(np.sum(ext_ok & (dl <= 1e-6)))}
     for name in dict.fromkeys(names):
         m = np.array([nm == name for nm in names] + [False] * (len(lanes) - len(names)))
         out[name] = {"lanes": int(m.sum()), "ext_stable": int(np.sum(m & ext_ok)),
@@ -306,6 +316,12 @@ def parity_leg(u0_gpu, x0, traj, sid, N, K, n, r, run, nlp, gpu_dev=None, qp_ite
         out["gpu_chaotic_frac"] = float(gc.mean())
         out["chaotic_overlap_jaccard"] = float((gc & rc).sum() / max(int((gc | rc).sum()), 1))
         out["frac_err_gt_1e-6_stable_in_both"] = float(np.mean((d > 1e-6) & ~gc & ~rc))
+        # the metric max|u0 - u0_ref| on the lanes stable under every probe of both implementations
+        # (x0 probes on the GPU; x0, mu_stop and model probes on the literal)
+        sb = (gpu_dev[:n] <= 1e-6) & (self_dev <= 1e-6) & (mod_dev <= 1e-6)
+        out["probe_stable_in_both"] = {"lanes": int(sb.sum()),
+                                       "max_abs_u0_err": float(d[sb].max()) if sb.any() else None,
+                                       "frac_err_le_1e-6": float(np.mean(d[sb] <= 1e-6)) if sb.any() else None}
     if extended:
         # the disagreements adjudicated in extended precision: first the lanes stable in both
         # implementations, then those the literal's probes call stable, then the others
@@ -722,22 +738,27 @@ def main():
                      "whole_solve_tflops": flops_solve / avg_kern_s / 1e12},
     }
     result["device"] = device_facts(dev)
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    # HBM traffic per launch from the PMC record of this workload (profiles/pmc_traffic*.json: the
+    # headline's and configs[4]'s), only while the library is built from the kernel code it was
+    # collected at
+    import glob
+    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")))
+    if recs:
+        result["roofline"]["traffic_source"] = ("not reported: no profiles/pmc_traffic*.json record of this "
+                                                "kernel source and workload")
         try:
-            with open(pmc) as f:
-                pm = json.load(f)
             from uclv_qs_pushing_matlab_amd.build import source_digest
-            same_kernel = pm.get("kernel_digest") == source_digest()
-            if (same_kernel and pm.get("batch") == Bl and pm.get("N") == N and pm.get("sqp_iters") == K
-                    and pm.get("qp_iters", 20) == args.qp_iters):
-                result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-                result["roofline"]["traffic_source"] = ("profiles/pmc_traffic.json: rocprofv3 FETCH_SIZE x 2 + "
-                                                        "WRITE_SIZE of this kernel source (digest "
-                                                        f"{pm.get('kernel_digest')})")
-            else:
-                result["roofline"]["traffic_source"] = ("not reported: profiles/pmc_traffic.json was collected "
-                                                        "for another kernel source or workload")
+            dig = source_digest()
+            for path in recs:
+                with open(path) as f:
+                    pm = json.load(f)
+                if (pm.get("kernel_digest") == dig and pm.get("batch") == Bl and pm.get("N") == N
+                        and pm.get("sqp_iters") == K and pm.get("qp_iters", 20) == args.qp_iters):
+                    result["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+                    result["roofline"]["traffic_source"] = (f"profiles/{os.path.basename(path)}: rocprofv3 FETCH_SIZE x 2 "
+                                                            "+ WRITE_SIZE of this kernel source (digest "
+                                                            f"{pm.get('kernel_digest')})")
+                    break
         except Exception:
             pass
 
@@ -863,6 +884,19 @@ def main():
         # restatement, and how the disagreements that survive every probe are adjudicated in __float128
         ep = pl.get("extended_precision", {})
         sb = ep.get("stable_in_both", {})
+        ps = pl.get("probe_stable_in_both", {})
+        es = ep.get("extended_stable", {})
+        # the metric max|u0 - u0_ref| against the independent restatement, on three strata, at the top of
+        # `parity` (max_abs_u0_err above is against the twin, a consistency check of the kernel's order)
+        result["parity"]["max_abs_u0_err_vs_twin"] = result["parity"]["max_abs_u0_err"]
+        result["parity"]["max_abs_u0_err_vs_literal"] = {
+            "all_lanes": {"lanes": pl["lanes"], "max": pl["max_abs_u0_err"], "frac_le_1e-6": pl["frac_lanes_err_le_1e-6"]},
+            "probe_stable_in_both": {"lanes": ps.get("lanes"), "max": ps.get("max_abs_u0_err"),
+                                     "frac_le_1e-6": ps.get("frac_err_le_1e-6")},
+            "extended_stable_vs_quad": {"lanes": es.get("lanes", 0), "max": es.get("max_abs_u0_err_gpu_vs_quad"),
+                                        "literal_max": es.get("max_abs_u0_err_literal_vs_quad"),
+                                        "note": "adjudicated sample only (disagreeing lanes first, then agreeing "
+                                                "controls) where long double and __float128 agree to 1e-6: u0_ref = quad"}}
         result["parity"]["independent"] = {
             "reference": "oracle/qsp_oracle.c (literal restatement), adjudicated by its __float128 build",
             "lanes": pl["lanes"], "frac_within_1e-6": pl["frac_lanes_err_le_1e-6"],

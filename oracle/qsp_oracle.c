@@ -71,6 +71,7 @@ typedef double real;
 #define NDIR 6 /* AD directions: x, y, theta, s, u_n, u_t */
 #define OR_MAX_N 128
 #define OR_MAX_CTRL 256
+#define OR_KKT_DIAG 22   /* doubles per lane of or_set_kkt_diag */
 
 /* ------------------------------------------------------------------ shapes */
 typedef struct {
@@ -666,17 +667,23 @@ typedef struct {
     int qp_capped;   /* QPs of this solve stopped by the iteration cap */
     int qp_stalled;  /* ... by the stall exit */
     uint32_t mode[OR_MAX_N];  /* motion-cone modes of the stages' RK4 evaluations (diagnostics) */
-    real kkt[18];  /* diagnostics of the last NLP KKT test (nlp_mode 1): see or_set_kkt_diag */
+    real kkt[OR_KKT_DIAG];  /* diagnostics of the NLP KKT tests (nlp_mode 1): see or_set_kkt_diag */
 } or_ws;
 
-/* KKT diagnostics (nlp_mode 1), per lane 18 doubles: the residuals of the last KKT test the SQP
+/* KKT diagnostics (nlp_mode 1), per lane OR_KKT_DIAG = 22 doubles: the residuals of the last KKT test the SQP
  * evaluated -- u-stationarity, x-stationarity (stages 1..N-1), terminal stationarity, equality,
  * inequality, complementarity -- then the SQP iteration of that test, the last line-search
  * step length, that line search's directional derivative, merit at alpha = 0 and at the last step
  * tried, the number of line searches that ended at ls_alpha_min; for the last QP its exit code,
  * the term sum r_u' du of its u-stationarity residual r_u, -d'Hd, and sum pi'b - nu|b|; the number
  * of stages whose motion-cone modes (at the four RK4 evaluations) changed between the last two
- * linearisations, and over all linearisations from SQP iteration 10 on.  NULL: off. */
+ * linearisations, and over all linearisations from SQP iteration 10 on; the tolerance margin of
+ * the solve's decisions: over every KKT test it evaluated, the smallest |log10 q| with q = max of
+ * res_stat/tol_stat, res_eq/tol_eq, res_ineq/tol_ineq, res_comp/tol_comp (q < 1 passes), and the q
+ * of that closest test.  A solve whose margin exceeds 1 never had a residual within a factor 10 of
+ * its tolerance at any decision; the line searches' margin: over every Armijo test of the solve,
+ * the smallest |phi(alpha) - phi0 - eps alpha dphi| / |phi0|, and the SQP iteration of that test (a
+ * test whose two sides agree to rounding is decided by rounding).  NULL: off. */
 static real *g_kkt_diag = NULL;
 OR_EXPORT void or_set_kkt_diag(real *buf) { g_kkt_diag = buf; }
 
@@ -740,6 +747,8 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const real x0[4],
     memset(eta, 0, sizeof(real) * 6 * N);
     int it;
     memset(ws->kkt, 0, sizeof ws->kkt);
+    ws->kkt[18] = 1e300;
+    ws->kkt[20] = 1e300;
     if (o->nlp_mode == 1) status = 2;
     /* stage-0 s bound: s_0 = x0's s is fixed in every QP; outside [lh_s, uh_s] all of them are
      * infeasible and the solve stops before its first iteration (status 4, ACADOS_QP_FAILURE) */
@@ -819,6 +828,14 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const real x0[4],
             }
             ws->kkt[0] = r_u; ws->kkt[1] = r_x; ws->kkt[3] = r_eq; ws->kkt[4] = r_ineq; ws->kkt[5] = r_comp;
             ws->kkt[6] = it;
+            {
+                real q = r_stat / o->tol_stat;
+                if (r_eq / o->tol_eq > q) q = r_eq / o->tol_eq;
+                if (r_ineq / o->tol_ineq > q) q = r_ineq / o->tol_ineq;
+                if (r_comp / o->tol_comp > q) q = r_comp / o->tol_comp;
+                const double qd = (double)q, mg = qd > 0.0 ? (qd >= 1.0 ? log10(qd) : -log10(qd)) : 1e300;
+                if (mg < (double)ws->kkt[18]) { ws->kkt[18] = mg; ws->kkt[19] = q; }
+            }
             if (r_stat < o->tol_stat && r_eq < o->tol_eq && r_ineq < o->tol_ineq && r_comp < o->tol_comp) {
                 status = 0;
                 break;
@@ -884,6 +901,11 @@ static int sqp_solve(const or_shape *sh, const or_opts *o, const real x0[4],
                 for (int q = 0; q < 2 * N; ++q) Ut[q] = U[q] + alpha * ws->du[q];
                 real phi = merit_eval(sh, o, Xt, Ut, yref, yref_e, nu, eta);
                 ws->kkt[10] = phi;
+                {
+                    const real gap = phi - (phi0 + o->ls_eps * alpha * dphi);
+                    const double rel = (double)(fabs(gap) / (fabs(phi0) > 1e-300 ? fabs(phi0) : 1e-300));
+                    if (rel < (double)ws->kkt[20]) { ws->kkt[20] = rel; ws->kkt[21] = it; }
+                }
                 if (phi <= phi0 + o->ls_eps * alpha * dphi) break;
                 real an = alpha * o->ls_alpha_red;
                 if (an < ((g_exp & 4) ? 1e-12 : o->ls_alpha_min)) { ws->kkt[11] += 1.0; break; }   /* accept the last step tried */
@@ -1035,7 +1057,7 @@ OR_EXPORT int or_ocp_solve(const int32_t *n_ctrl, const real *ctrl, const real *
             if (qp_iter) qp_iter[i] = ws->qp_total;
             if (qp_capped) qp_capped[i] = ws->qp_capped;
             if (qp_stalled) qp_stalled[i] = ws->qp_stalled;
-            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)18 * i, ws->kkt, sizeof ws->kkt);
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)OR_KKT_DIAG * i, ws->kkt, sizeof ws->kkt);
             cost[i] = ocp_cost(o, N, Xi, Ui, yr, ye);
         }
         free(ws);
@@ -1152,7 +1174,7 @@ OR_EXPORT int or_controller_solve(const int32_t *n_ctrl, const real *ctrl, const
                                         Xw + (size_t)i * 4 * (N + 1), Uw + (size_t)i * 2 * N, PIw + (size_t)i * 4 * N,
                                         warm_valid + i, u0 + 2 * i, iters ? iters + i : NULL, qp_iter ? qp_iter + i : NULL,
                                         qp_capped ? qp_capped + i : NULL, cost + i, ws, qp_stalled ? qp_stalled + i : NULL);
-            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)18 * i, ws->kkt, sizeof ws->kkt);
+            if (g_kkt_diag) memcpy(g_kkt_diag + (size_t)OR_KKT_DIAG * i, ws->kkt, sizeof ws->kkt);
         }
         free(ws);
     }

@@ -38,3 +38,24 @@ def test_extended_adjudication_sides_with_the_gpu_on_the_stable_lane():
     sb = out["stable_in_both"]
     assert sb["lanes"] == 1 and sb["sides_with_gpu"] == 1 and sb["ext_stable"] == 1
     assert sb["per_lane"][0]["gpu_err"] < 1e-12 and sb["per_lane"][0]["literal_err"] > 0.09
+
+
+def test_parity_leg_strata():
+    """The bench line's independent parity: max|u0 - u0_ref| against the literal restatement on all
+    lanes, on the lanes stable under every probe of both implementations, and against __float128 on the
+    extended-stable adjudicated lanes (the twin standing in for the device)."""
+    import bench
+    n, K = 12, 6
+    x0, _, _, sid, traj = bench.make_inputs(n, 20, bench.SEED)
+    _, _, rt, run_t = bench.cpu_baseline(x0, traj, sid, 20, K, 0.0, 2, sample=n)
+    _, _, rl, run_l = bench.cpu_baseline(x0, traj, sid, 20, K, 0.0, 2, twin=False, sample=n)
+    gdev = np.zeros(n)
+    for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):
+        gdev = np.maximum(gdev, np.abs(run_t(slice(0, n), x0 * (1 + sgn * f * 1e-13))["u0"] - rt["u0"]).max(1))
+    pl = bench.parity_leg(rt["u0"], x0, traj, sid, 20, K, n, rl, run_l, "SQP_RTI", gdev, ext_lanes=4)
+    d = np.abs(rt["u0"] - rl["u0"]).max(1)
+    assert pl["max_abs_u0_err"] == d.max()
+    ps = pl["probe_stable_in_both"]
+    assert 0 < ps["lanes"] <= n and ps["max_abs_u0_err"] <= d.max()
+    es = pl["extended_precision"].get("extended_stable")
+    assert es is None or (es["lanes"] >= 1 and es["max_abs_u0_err_gpu_vs_quad"] >= 0.0)

@@ -31,7 +31,7 @@ def literal_run(B, exp=0):
     orc = Oracle(NAMES)
     x0, _, _, sid, traj = make_inputs(B, 20, SEED + 7)
     op = make_opts(N=20, sqp_iters=30, nlp_mode=1, qp_iters=50)
-    diag = np.zeros((B, 18))
+    diag = np.zeros((B, 22))
     lib().or_set_kkt_diag(diag.ctypes.data_as(C.c_void_p))
     lib().or_set_experiment(C.c_int(exp))
     try:
@@ -87,3 +87,35 @@ def test_closed_loop_breakdown():
     f = b["status2_fail_frac"]
     assert f["stat"] > 0.7 and f["eq"] > 0.5 and f["ineq"] < 0.05
     assert set(b["status"]) <= {0, 2, 4}
+
+
+def test_merit_literal_strata_twin():
+    """The strata of tests/test_gpu_merit.py's literal parity, with the twin standing in for the device
+    (they are equal bit for bit, tests/test_gpu_twin.py): on 384 lanes of its hardest block, the far
+    stratum agrees with the literal in status and sqp_iter on every lane, at both controller steps."""
+    from bench import SEED, make_inputs
+    from merit_strata import check_step, literal_two_steps
+    from oracle.oracle import Oracle, make_opts
+    names = ("santal", "balea", "montana", "pulirapid")
+    lit, tw = Oracle(names), Oracle(names, twin=True)
+    N, nb = 20, 384
+    x0a, _, _, sida, traj = make_inputs(4096, N, SEED + 7)
+    x0, sid = x0a[3072:3072 + nb], sida[3072:3072 + nb]
+    op = make_opts(N=N, sqp_iters=30, nlp_mode=1, qp_iters=50)
+    r1, r2, x1, strata = literal_two_steps(lit, op, x0, sid, traj)
+    warm = tw.new_warm(nb, N)
+    t1 = tw.controller_solve(op, x0, traj, 1, warm, shape_id=sid)
+    t2 = tw.controller_solve(op, x1, traj, 2, warm, shape_id=sid)
+    import merit_strata
+    for t, r, k in ((t1, r1, 1), (t2, r2, 2)):
+        far = strata[f"far{k}"]
+        assert far.sum() >= 80, far.sum()
+        neq = (t["status"] != r["status"]) | (t["iters"] != r["iters"])
+        assert not np.any(neq & far), np.flatnonzero(neq & far)
+        # every status/sqp_iter difference among the probe-stable lanes is an edge decision
+        edge = strata[f"stable{k}"] & ~far & neq
+        km, am = strata["kkt_margin"][k - 1], strata["armijo_margin"][k - 1]
+        if k == 2:
+            km = np.minimum(km, strata["kkt_margin"][0])
+            am = np.minimum(am, strata["armijo_margin"][0])
+        assert np.all((km[edge] <= merit_strata.KKT_DECADES) | (am[edge] <= merit_strata.ARMIJO_REL))

@@ -23,7 +23,7 @@ def run(impl, B, K, steps, qp_iters, tol, **kw):
     x0, _, _, sid, traj = make_inputs(B, 20, SEED + 7)
     op = make_opts(N=20, sqp_iters=K, nlp_mode=1, qp_iters=qp_iters, tol=tol, **kw)
     warm = orc.new_warm(B, 20)
-    diag = np.zeros((B, 18 if impl == 'literal' else 8))
+    diag = np.zeros((B, 22 if impl == 'literal' else 8))
     setter = getattr(orc.L, ("tw_" if impl == "twin" else "or_") + "set_kkt_diag")
     setter(diag.ctypes.data_as(C.c_void_p))
     out = []

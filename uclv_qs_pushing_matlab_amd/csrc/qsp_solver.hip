@@ -40,6 +40,9 @@
 #ifndef QSP_MIN_WAVES
 #define QSP_MIN_WAVES 1
 #endif
+#ifndef QSP_S2_SCAN_FACTOR
+#define QSP_S2_SCAN_FACTOR 0
+#endif
 
 namespace qsp {
 
@@ -440,6 +443,137 @@ __device__ __forceinline__ void aff_delta(const double a[6], const double B[8], 
     }
 }
 
+// ---------------------------------- S = 2: the factorisation as an associative scan
+// The conditional value-function element of a stage (Sarkka & Garcia-Fernandez, "Temporal
+// parallelization of dynamic programming and linear quadratic control", IEEE TAC 2023):
+//   e_k = (A, b, C, eta, J) = (A_k, c_k - B Hu^-1 gu, B Hu^-1 B', -gx, diag Hx),
+//   e_N = (0, 0, 0, -g_N, We);
+// combining e_ij with e_jk (M = (I + C_ij J_jk)^-1):
+//   A = A_jk M A_ij, b = A_jk M (b_ij + C_ij eta_jk) + b_jk, C = A_jk M C_ij A_jk' + C_jk,
+//   eta = A_ij' M' (eta_jk - J_jk b_ij) + eta_ij, J = A_ij' M' J_jk A_ij + J_ij.
+// The suffix product over stages k..N holds the value function of stage k: P_k = J, p_k = -eta.
+// (scripts/ubench/riccati_scan_s2.hip: 0.125 ms vs the walk's 0.149 ms per factorisation of the
+// configs[4] batch.)
+struct VElem { double A[16], b[4], C[10], eta[4], J[10]; };
+constexpr int VELEM_N = 44;
+
+__device__ __forceinline__ void velem_stage(const double a[6], const double B[8], const double bb[4], const double Hx[4],
+                                            const double Hu[2], const double gx[4], const double gu[2], VElem& e) {
+    const double F[16] = {1.0, 0.0, a[0], a[1], 0.0, 1.0, a[2], a[3], 0.0, 0.0, 1.0, a[4], 0.0, 0.0, 0.0, a[5]};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e.A[q] = F[q];
+    const double ih0 = rcp(Hu[0]), ih1 = rcp(Hu[1]);
+    const double v0 = ih0 * gu[0], v1 = ih1 * gu[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        e.b[i] = qfma(-B[2 * i + 1], v1, qfma(-B[2 * i], v0, bb[i]));
+        e.eta[i] = -gx[i];
+        const double w0 = B[2 * i] * ih0, w1 = B[2 * i + 1] * ih1;
+#pragma unroll
+        for (int j = i; j < 4; ++j) {
+            e.C[sidx(i, j)] = qfma(w1, B[2 * j + 1], w0 * B[2 * j]);
+            e.J[sidx(i, j)] = (i == j) ? Hx[i] : 0.0;
+        }
+    }
+}
+__device__ __forceinline__ void velem_terminal(const double We[4], const double g[6], VElem& e) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e.A[q] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) { e.C[q] = 0.0; e.J[q] = 0.0; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { e.b[q] = 0.0; e.eta[q] = -g[q]; e.J[sidx(q, q)] = We[q]; }
+}
+// e <- e (x) f  (e the earlier stages, f the later ones), in place
+__device__ __forceinline__ void velem_combine(VElem& e, const VElem& f) {
+    // T = I + C_ij J_jk, inverted in place by Gauss-Jordan without pivoting (C, J symmetric positive
+    // semidefinite: the eigenvalues of I + C J are >= 1)
+    double T[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            T[i][j] = qfma(e.C[sidx(i, 3)], f.J[sidx(3, j)], qfma(e.C[sidx(i, 2)], f.J[sidx(2, j)],
+                      qfma(e.C[sidx(i, 1)], f.J[sidx(1, j)], qfma(e.C[sidx(i, 0)], f.J[sidx(0, j)], i == j ? 1.0 : 0.0))));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double piv = rcp(T[c][c]);
+        T[c][c] = 1.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) T[c][j] *= piv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            const double fct = T[r][c];
+            T[r][c] = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) T[r][j] = qfma(-fct, T[c][j], T[r][j]);
+        }
+    }
+    // TA = A_jk M ; U = A_ij' M'
+    double TA[4][4], Um[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            TA[i][j] = qfma(f.A[4 * i + 3], T[3][j], qfma(f.A[4 * i + 2], T[2][j], qfma(f.A[4 * i + 1], T[1][j], f.A[4 * i] * T[0][j])));
+            Um[i][j] = qfma(e.A[12 + i], T[j][3], qfma(e.A[8 + i], T[j][2], qfma(e.A[4 + i], T[j][1], e.A[i] * T[j][0])));
+        }
+    // w = b_ij + C_ij eta_jk ; z = eta_jk - J_jk b_ij
+    double w[4], z[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w[i] = qfma(e.C[sidx(i, 3)], f.eta[3], qfma(e.C[sidx(i, 2)], f.eta[2], qfma(e.C[sidx(i, 1)], f.eta[1], qfma(e.C[sidx(i, 0)], f.eta[0], e.b[i]))));
+        z[i] = qfma(-f.J[sidx(i, 3)], e.b[3], qfma(-f.J[sidx(i, 2)], e.b[2], qfma(-f.J[sidx(i, 1)], e.b[1], qfma(-f.J[sidx(i, 0)], e.b[0], f.eta[i]))));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        e.b[i] = qfma(TA[i][3], w[3], qfma(TA[i][2], w[2], qfma(TA[i][1], w[1], qfma(TA[i][0], w[0], f.b[i]))));
+        e.eta[i] = qfma(Um[i][3], z[3], qfma(Um[i][2], z[2], qfma(Um[i][1], z[1], qfma(Um[i][0], z[0], e.eta[i]))));
+    }
+    // J = (U J_jk) A_ij + J_ij  (needs the old A_ij: before A is replaced)
+    {
+        double Y[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                Y[i][j] = qfma(Um[i][3], f.J[sidx(3, j)], qfma(Um[i][2], f.J[sidx(2, j)], qfma(Um[i][1], f.J[sidx(1, j)], Um[i][0] * f.J[sidx(0, j)])));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j)
+                e.J[sidx(i, j)] = qfma(Y[i][3], e.A[12 + j], qfma(Y[i][2], e.A[8 + j], qfma(Y[i][1], e.A[4 + j], qfma(Y[i][0], e.A[j], e.J[sidx(i, j)]))));
+    }
+    // C = (TA C_ij) A_jk' + C_jk
+    {
+        double X[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                X[i][j] = qfma(TA[i][3], e.C[sidx(3, j)], qfma(TA[i][2], e.C[sidx(2, j)], qfma(TA[i][1], e.C[sidx(1, j)], TA[i][0] * e.C[sidx(0, j)])));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j)
+                e.C[sidx(i, j)] = qfma(X[i][3], f.A[4 * j + 3], qfma(X[i][2], f.A[4 * j + 2], qfma(X[i][1], f.A[4 * j + 1], qfma(X[i][0], f.A[4 * j], f.C[sidx(i, j)]))));
+    }
+    // A = TA A_ij, column by column (column j of the result needs column j of A_ij only)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const double c0 = e.A[j], c1 = e.A[4 + j], c2 = e.A[8 + j], c3 = e.A[12 + j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e.A[4 * i + j] = qfma(TA[i][3], c3, qfma(TA[i][2], c2, qfma(TA[i][1], c1, TA[i][0] * c0)));
+    }
+}
+__device__ __forceinline__ void velem_read(const VElem& e, int src, VElem& f) {
+    const double* s = &e.A[0];
+    double* d = &f.A[0];
+#pragma unroll
+    for (int q = 0; q < VELEM_N; ++q) d[q] = lane_read(s[q], src);
+}
+
 // ------------------------------------------------------------------ QP core
 // Barrier terms of slot ls into LDS (predictor): hg[0..2] Hessian additions, hg[3..5]
 // gradient additions.  The corrector changes only the gradient (corrector_terms).
@@ -677,6 +811,58 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvs, dkk);
                 st.kk[ls][0] += dkk[0];
                 st.kk[ls][1] += dkk[1];
+            }
+        }
+    } else if constexpr (S == 2 && FACTOR && QSP_S2_SCAN_FACTOR) {
+        // factorisation as a suffix scan of the lanes' value-function elements: lane j combines its
+        // two stages' elements (slot 0's, then slot 1's; the terminal element where k = N, none past
+        // it), Hillis-Steele levels give E_{2j:N}, the next lane's result E_{2j+2:N} gives slot 1's
+        // E_{2j+1:N}; then each slot forms K, Rn, kk from its successor's value function
+        const int k0 = 2 * c.lig, k1 = k0 + 1;
+        VElem e, e1;
+        {
+            const double Hx0[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
+            const double gxa[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
+            if (k0 < c.N) velem_stage(st.a[0], st.B[0], st.bb[0], Hx0, hu[0], gxa, gu[0], e);
+            else velem_terminal(p.We, st.g[0], e);
+            const double Hx1[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
+            const double gxb[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
+            if (k1 < c.N) velem_stage(st.a[1], st.B[1], st.bb[1], Hx1, hu[1], gxb, gu[1], e1);
+            else velem_terminal(p.We, st.g[1], e1);
+            if (k1 <= c.N) {
+                VElem t = e1;
+                velem_combine(e, t);
+            }
+        }
+        for (int off = 1; off < c.L; off <<= 1) {
+            const bool take = c.lig + off < c.L;
+            VElem f;
+            velem_read(e, take ? c.lane + off : c.lane, f);
+            if (take) velem_combine(e, f);
+        }
+        {
+            VElem f;
+            velem_read(e, c.lig + 1 < c.L ? c.lane + 1 : c.lane, f);
+            if (k1 < c.N) {
+                velem_combine(e1, f);
+                double Pn[10], pn[4];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) Pn[q] = f.J[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pn[q] = -f.eta[q];
+                const double gx[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
+                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
+                ric_factor_step(st.a[1], st.B[1], st.bb[1], Hx, hu[1], gx, gu[1], Pn, pn, st.K[1], st.Rn[1], st.kk[1], false);
+            }
+            if (k0 < c.N) {
+                double Pn[10], pn[4];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) Pn[q] = e1.J[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pn[q] = -e1.eta[q];
+                const double gx[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
+                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
+                ric_factor_step(st.a[0], st.B[0], st.bb[0], Hx, hu[0], gx, gu[0], Pn, pn, st.K[0], st.Rn[0], st.kk[0], false);
             }
         }
     } else
