@@ -537,6 +537,8 @@ def main():
                          "-2.2 %% here, but 2.3x slower at B = 4 096 where every SQP iteration waits for its slowest "
                          "wave; DESIGN.md section 1)")
     ap.add_argument("--stages-per-lane", type=int, default=0)
+    ap.add_argument("--factor-scan", action="store_true",
+                    help="two stages per lane: the factorisation as an associative scan (qsp_options.factor_scan)")
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
                     help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -601,7 +603,7 @@ def main():
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
-                       device=gpu, nlp_solver_type=args.nlp)
+                       device=gpu, nlp_solver_type=args.nlp, factor_scan=args.factor_scan)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
     solver.set_stream_parts(args.stream_parts)
@@ -720,7 +722,7 @@ def main():
                    "global_batch": total, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
                    "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
-                              "stream_parts": parts},
+                              "stream_parts": parts, "factor_scan": bool(args.factor_scan and S_layout == 2)},
                    "parallelism": f"dp{world} (contiguous lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
@@ -828,6 +830,24 @@ def main():
                               "layout": {"stages_per_lane": S4, "lanes_per_instance": L4},
                               "note": "host-boundary controller solves (x0 in, u0 out), 3 repeats"}
         u4_gpu = s4.get_u0()
+        # the factorisation-scan option (qsp_options.factor_scan) on the same workload: its rate, and its
+        # u0 against the default's (it rounds differently: two digits less accurate)
+        s4s = OcpSolver(N=50, batch=len(x4), sqp_iters=K, qp_iters=args.qp_iters, device=gpu, factor_scan=True)
+        s4s.set_shapes([make_shape(n) for n in SHAPES])
+        s4s.set_shape_ids(sid4)
+        s4s.set_reference_trajectory(traj4)
+        s4s.controller_solve(x4, idx4b)
+        s4s.synchronize()
+        t4s = time.perf_counter()
+        for _ in range(3):
+            s4s.controller_reset()
+            u4_scan = s4s.controller_solve(x4, idx4b)
+        s4s.synchronize()
+        dsc = np.abs(u4_scan - u4_gpu).max(1)
+        result["configs4"]["factor_scan"] = {"gpu_solves_per_s": len(x4) * 3 / (time.perf_counter() - t4s),
+                                             "frac_u0_within_1e-6_of_default": float(np.mean(dsc <= 1e-6)),
+                                             "status_equal_lanes": int(np.sum(s4s.get("status") == s4.get("status")))}
+        s4s.close()
         # the GPU's own response to the literal parity leg's 1e-13 x0 probes (untimed)
         gpu_dev4 = np.zeros(len(x4))
         for sgn, f in ((1, 1.0), (-1, 1.0), (1, 3.0)):

@@ -35,6 +35,21 @@ def lib():
     return _lib
 
 
+def _threads(n):
+    """OpenMP threads of a call: n, or (n = 0) the job's share -- OMP_NUM_THREADS, else the CPUs of the
+    affinity mask.  Always explicit, because omp_set_num_threads persists in the process: a call
+    with n = 1 (a thread-scaling sample) would otherwise leave every later call on one thread."""
+    if n and n > 0:
+        return int(n)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 class Opts(C.Structure):
     _fields_ = [
         ("N", C.c_int32), ("sqp_iters", C.c_int32), ("qp_iters", C.c_int32), ("stage0_s_bound", C.c_int32),
@@ -51,7 +66,7 @@ class Opts(C.Structure):
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
         ("qp_stall_alpha", C.c_double), ("qp_stall_iters", C.c_int32), ("stages_per_lane", C.c_int32),
         ("qp_mu_max", C.c_double),
-        ("model_probe", C.c_double), ("probe_seed", C.c_int32), ("pad2_", C.c_int32),
+        ("model_probe", C.c_double), ("probe_seed", C.c_int32), ("factor_scan", C.c_int32),
     ]
 
 
@@ -61,13 +76,14 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
               mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
               u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
               qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1, qp_stall_alpha=1e-3, qp_stall_iters=3,
-              qp_mu_max=1e100, stages_per_lane=0, model_probe=0.0, probe_seed=0):
+              qp_mu_max=1e100, stages_per_lane=0, model_probe=0.0, probe_seed=0, factor_scan=0):
     o = Opts()
     o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, int(stage0_s_bound)
     o.qp_tol_stat, o.qp_tol_eq = qp_tol_stat, qp_tol_eq
     o.qp_stall_alpha, o.qp_stall_iters = qp_stall_alpha, int(qp_stall_iters)
     o.qp_mu_max, o.stages_per_lane = qp_mu_max, int(stages_per_lane)
     o.model_probe, o.probe_seed = float(model_probe), int(probe_seed)
+    o.factor_scan = int(factor_scan)
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W
@@ -192,7 +208,7 @@ class Oracle:
         stalled = np.zeros(nb, np.int32)
         self._f("ocp_solve")(*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(yref), _p(yref_e),
                              _p(X), _p(U), _p(PI), _p(lam), _p(status), _p(iters), _p(qp_iter), _p(cost),
-                             C.c_int(nthreads), _p(capped), _p(stalled))
+                             C.c_int(_threads(nthreads)), _p(capped), _p(stalled))
         return dict(X=X, U=U, PI=PI, lam=lam, status=status, iters=iters, qp_iter=qp_iter, cost=cost, qp_capped=capped,
                     qp_stalled=stalled)
 
@@ -218,7 +234,7 @@ class Oracle:
         stalled = np.zeros(nb, np.int32)
         args = [*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj), C.c_int32(T), _p(idx),
                 _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]), _p(warm["valid"]), _p(u0), _p(status), _p(iters),
-                _p(qp_iter), _p(cost), C.c_int(nthreads), _p(capped), C.c_int32(int(delay_cols))]
+                _p(qp_iter), _p(cost), C.c_int(_threads(nthreads)), _p(capped), C.c_int32(int(delay_cols))]
         if self.twin:
             self.L.tw_controller_solve(*args, C.c_int32(int(per_lane)), _p(stalled))
         else:
@@ -245,7 +261,7 @@ class Oracle:
         fn = {"long": self.L.orx_controller_solve_l, "quad": self.L.orx_controller_solve_q}[precision]
         r = fn(*self._shape_args(), C.c_int32(len(self._n)), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
                C.c_int32(len(traj)), _p(idx), _p(warm["X"]), _p(warm["U"]), _p(warm["PI"]), _p(warm["valid"]), _p(u0),
-               _p(status), _p(iters), _p(qp_iter), _p(cost), C.c_int(nthreads), C.c_int32(int(delay_cols)))
+               _p(status), _p(iters), _p(qp_iter), _p(cost), C.c_int(_threads(nthreads)), C.c_int32(int(delay_cols)))
         if r != 0:
             raise ValueError("orx_controller_solve: bad arguments")
         return dict(u0=u0, status=status, iters=iters, qp_iter=qp_iter, cost=cost)
@@ -269,7 +285,7 @@ class Oracle:
         args = [*self._shape_args(), C.byref(opts), C.c_int32(nb), _p(sid), _p(x0), _p(traj),
                 C.c_int32(len(traj)), _p(idx), C.c_int32(n), None if nz is None else _p(nz),
                 C.c_int32(int(delay_cols)), C.c_int32(int(plant_delay_cols)), C.c_int32(int(dist_step)),
-                _p(amp), _p(xw), _p(X), _p(Xs), _p(U), _p(st), C.c_int(nthreads)]
+                _p(amp), _p(xw), _p(X), _p(Xs), _p(U), _p(st), C.c_int(_threads(nthreads))]
         if self.twin:   # ubc0: the controller's input buffer at the start (B x delay_cols x 2; None: zeros)
             u0b = None if ubc0 is None else np.ascontiguousarray(ubc0, np.float64).reshape(nb, int(delay_cols), 2)
             r = self.L.tw_closed_loop(*args, None if u0b is None else _p(u0b))

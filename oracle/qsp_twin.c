@@ -356,7 +356,7 @@ typedef struct {
 
 /* the solve parameters the kernels read (SolveParams): the options plus the QP-level overrides */
 typedef struct {
-    int N, S, L, nlp_mode, sqp_iters, qp_iters, qp_stall_iters, s0_bound;
+    int N, S, L, nlp_mode, sqp_iters, qp_iters, qp_stall_iters, s0_bound, factor_scan;
     double Ts, tau, W[6], We[4], lh[3], uh[3];
     double mu0, t_min, frac, sigma_min, mu_stop, res_stop, qp_tol_stat, qp_tol_eq, qp_stall_alpha, qp_mu_max;
     double tol_stat, tol_eq, tol_ineq, tol_comp, ls_alpha_min, ls_alpha_red, ls_eps;
@@ -381,6 +381,7 @@ static void make_par(tw_par *p, const or_opts *o)
     p->qp_iters = o->qp_iters;
     p->qp_stall_iters = o->qp_stall_iters;
     p->s0_bound = o->stage0_s_bound ? 1 : 0;
+    p->factor_scan = o->factor_scan ? 1 : 0;
     p->Ts = o->Ts;
     p->tau = o->tau;
     memcpy(p->W, o->W, sizeof p->W);
@@ -754,6 +755,146 @@ static void forward_scan_s2(const tw_par *p, tw_stage *st, const double dx0[4], 
     }
 }
 
+/* ---- S = 2: the factorisation as an associative scan (qsp_solver.hip VElem, velem_*; riccati_solve<2, true>):
+ * the conditional value-function elements of Sarkka & Garcia-Fernandez (IEEE TAC 2023),
+ * e_k = (A_k, c_k - B Hu^-1 gu, B Hu^-1 B', -gx, diag Hx), e_N = (0, 0, 0, -g_N, We), combined in
+ * the kernel's association order; P_k = J, p_k = -eta of the suffix product over k..N */
+typedef struct { double A[16], b[4], C[10], eta[4], J[10]; } tw_velem;
+
+static void velem_stage(const double a[6], const double B[8], const double bb[4], const double Hx[4], const double Hu[2],
+                        const double gx[4], const double gu[2], tw_velem *e)
+{
+    const double F[16] = {1.0, 0.0, a[0], a[1], 0.0, 1.0, a[2], a[3], 0.0, 0.0, 1.0, a[4], 0.0, 0.0, 0.0, a[5]};
+    memcpy(e->A, F, sizeof F);
+    const double ih0 = rcp(Hu[0]), ih1 = rcp(Hu[1]);
+    const double v0 = ih0 * gu[0], v1 = ih1 * gu[1];
+    for (int i = 0; i < 4; ++i) {
+        e->b[i] = qfma(-B[2 * i + 1], v1, qfma(-B[2 * i], v0, bb[i]));
+        e->eta[i] = -gx[i];
+        const double w0 = B[2 * i] * ih0, w1 = B[2 * i + 1] * ih1;
+        for (int j = i; j < 4; ++j) {
+            e->C[sidx(i, j)] = qfma(w1, B[2 * j + 1], w0 * B[2 * j]);
+            e->J[sidx(i, j)] = (i == j) ? Hx[i] : 0.0;
+        }
+    }
+}
+static void velem_terminal(const double We[4], const double g[6], tw_velem *e)
+{
+    memset(e, 0, sizeof *e);
+    for (int q = 0; q < 4; ++q) { e->eta[q] = -g[q]; e->J[sidx(q, q)] = We[q]; }
+}
+/* e <- e (x) f in place (velem_combine) */
+static void velem_combine(tw_velem *e, const tw_velem *f)
+{
+    double T[4][4], TA[4][4], Um[4][4], w[4], z[4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            T[i][j] = qfma(e->C[sidx(i, 3)], f->J[sidx(3, j)], qfma(e->C[sidx(i, 2)], f->J[sidx(2, j)],
+                      qfma(e->C[sidx(i, 1)], f->J[sidx(1, j)], qfma(e->C[sidx(i, 0)], f->J[sidx(0, j)], i == j ? 1.0 : 0.0))));
+    for (int c = 0; c < 4; ++c) {
+        const double piv = rcp(T[c][c]);
+        T[c][c] = 1.0;
+        for (int j = 0; j < 4; ++j) T[c][j] *= piv;
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            const double fct = T[r][c];
+            T[r][c] = 0.0;
+            for (int j = 0; j < 4; ++j) T[r][j] = qfma(-fct, T[c][j], T[r][j]);
+        }
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            TA[i][j] = qfma(f->A[4 * i + 3], T[3][j], qfma(f->A[4 * i + 2], T[2][j], qfma(f->A[4 * i + 1], T[1][j], f->A[4 * i] * T[0][j])));
+            Um[i][j] = qfma(e->A[12 + i], T[j][3], qfma(e->A[8 + i], T[j][2], qfma(e->A[4 + i], T[j][1], e->A[i] * T[j][0])));
+        }
+    for (int i = 0; i < 4; ++i) {
+        w[i] = qfma(e->C[sidx(i, 3)], f->eta[3], qfma(e->C[sidx(i, 2)], f->eta[2], qfma(e->C[sidx(i, 1)], f->eta[1], qfma(e->C[sidx(i, 0)], f->eta[0], e->b[i]))));
+        z[i] = qfma(-f->J[sidx(i, 3)], e->b[3], qfma(-f->J[sidx(i, 2)], e->b[2], qfma(-f->J[sidx(i, 1)], e->b[1], qfma(-f->J[sidx(i, 0)], e->b[0], f->eta[i]))));
+    }
+    for (int i = 0; i < 4; ++i) {
+        e->b[i] = qfma(TA[i][3], w[3], qfma(TA[i][2], w[2], qfma(TA[i][1], w[1], qfma(TA[i][0], w[0], f->b[i]))));
+        e->eta[i] = qfma(Um[i][3], z[3], qfma(Um[i][2], z[2], qfma(Um[i][1], z[1], qfma(Um[i][0], z[0], e->eta[i]))));
+    }
+    {
+        double Y[4][4];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                Y[i][j] = qfma(Um[i][3], f->J[sidx(3, j)], qfma(Um[i][2], f->J[sidx(2, j)], qfma(Um[i][1], f->J[sidx(1, j)], Um[i][0] * f->J[sidx(0, j)])));
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j)
+                e->J[sidx(i, j)] = qfma(Y[i][3], e->A[12 + j], qfma(Y[i][2], e->A[8 + j], qfma(Y[i][1], e->A[4 + j], qfma(Y[i][0], e->A[j], e->J[sidx(i, j)]))));
+    }
+    {
+        double X[4][4];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j)
+                X[i][j] = qfma(TA[i][3], e->C[sidx(3, j)], qfma(TA[i][2], e->C[sidx(2, j)], qfma(TA[i][1], e->C[sidx(1, j)], TA[i][0] * e->C[sidx(0, j)])));
+        for (int i = 0; i < 4; ++i)
+            for (int j = i; j < 4; ++j)
+                e->C[sidx(i, j)] = qfma(X[i][3], f->A[4 * j + 3], qfma(X[i][2], f->A[4 * j + 2], qfma(X[i][1], f->A[4 * j + 1], qfma(X[i][0], f->A[4 * j], f->C[sidx(i, j)]))));
+    }
+    for (int j = 0; j < 4; ++j) {
+        const double c0 = e->A[j], c1 = e->A[4 + j], c2 = e->A[8 + j], c3 = e->A[12 + j];
+        for (int i = 0; i < 4; ++i) e->A[4 * i + j] = qfma(TA[i][3], c3, qfma(TA[i][2], c2, qfma(TA[i][1], c1, TA[i][0] * c0)));
+    }
+}
+
+/* the S = 2 factorisation: lane l combines its slots' elements, Hillis-Steele suffix levels over the
+ * lanes, slot 1's suffix from the next lane's result; each slot then forms K, Rn, kk from its
+ * successor's value function (ric_factor_step without the P update) */
+static void factor_scan_s2(const tw_par *p, tw_stage *st, const double *hx3, double (*hu)[2], const double *gx3,
+                           double (*gu)[2])
+{
+    const int N = p->N, L = p->L;
+    tw_velem e[64], ne[64], e1[64];
+    for (int l = 0; l < L; ++l) {
+        const int k0 = 2 * l, k1 = k0 + 1;
+        for (int ls = 0; ls < 2; ++ls) {
+            const int k = k0 + ls;
+            tw_velem *d = ls == 0 ? e + l : e1 + l;
+            if (k < N) {
+                const tw_stage *s = st + k;
+                const double Hx[4] = {p->tau * p->W[0], p->tau * p->W[1], p->tau * p->W[2], hx3[k]};
+                const double gx[4] = {s->g[0], s->g[1], s->g[2], gx3[k]};
+                velem_stage(s->a, s->B, s->bb, Hx, hu[k], gx, gu[k], d);
+            } else if (k == N) {
+                velem_terminal(p->We, st[N].g, d);
+            }
+        }
+        if (k1 <= N) velem_combine(e + l, e1 + l);
+    }
+    for (int off = 1; off < L; off <<= 1) {
+        for (int l = 0; l < L; ++l) {
+            ne[l] = e[l];
+            if (l + off < L) velem_combine(ne + l, e + l + off);
+        }
+        memcpy(e, ne, sizeof(tw_velem) * (size_t)L);
+    }
+    for (int l = 0; l < L; ++l) {
+        const int k0 = 2 * l, k1 = k0 + 1;
+        if (k1 < N) {
+            const tw_velem *f = e + l + 1;
+            velem_combine(e1 + l, f);
+            double Pn[10], pn[4];
+            for (int q = 0; q < 10; ++q) Pn[q] = f->J[q];
+            for (int q = 0; q < 4; ++q) pn[q] = -f->eta[q];
+            tw_stage *s = st + k1;
+            const double gx[4] = {s->g[0], s->g[1], s->g[2], gx3[k1]};
+            const double Hx[4] = {p->tau * p->W[0], p->tau * p->W[1], p->tau * p->W[2], hx3[k1]};
+            ric_factor_step(s->a, s->B, s->bb, Hx, hu[k1], gx, gu[k1], Pn, pn, s->K, s->Rn, s->kk, 0);
+        }
+        if (k0 < N) {
+            double Pn[10], pn[4];
+            for (int q = 0; q < 10; ++q) Pn[q] = e1[l].J[q];
+            for (int q = 0; q < 4; ++q) pn[q] = -e1[l].eta[q];
+            tw_stage *s = st + k0;
+            const double gx[4] = {s->g[0], s->g[1], s->g[2], gx3[k0]};
+            const double Hx[4] = {p->tau * p->W[0], p->tau * p->W[1], p->tau * p->W[2], hx3[k0]};
+            ric_factor_step(s->a, s->B, s->bb, Hx, hu[k0], gx, gu[k0], Pn, pn, s->K, s->Rn, s->kk, 0);
+        }
+    }
+}
+
 /* riccati_solve: factor (predictor) or the corrector's difference recursion, then the forward pass
  * writing the bounded solution components into VA (factor) / VN (corrector) */
 static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], int factor)
@@ -797,6 +938,8 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
         }
     } else if (S == 2 && !factor) {
         delta_scan_s2(p, st, gx3, gu);
+    } else if (S == 2 && factor && p->factor_scan) {
+        factor_scan_s2(p, st, hx3, hu, gx3, gu);
     } else {
         if (factor) {
             for (int i = 0; i < 10; ++i) P[i] = 0.0;

@@ -230,3 +230,18 @@ def test_closed_loop_composition(twin):
     ub = np.tile([0.01, 0.002], (nb, 2, 1))
     rb = twin.closed_loop(op, x0, traj, 2, shape_id=sid, delay_cols=2, ubc0=ub)
     assert not np.array_equal(rb["Xsim"][:, 0], rd["Xsim"][:, 0])
+
+
+def test_factor_scan_s2_matches_walk_at_one_iteration(twin):
+    """The S = 2 factorisation as an associative scan (factor_scan) against the walk at one SQP
+    iteration (the cold QP, before any amplification), N = 2 ... 127 with the terminal stage in either
+    slot.  Measured <= 1e-17: the scan's rounding (about two digits more than the walk's)
+    shows only once the SQP iterates."""
+    nb = 64
+    x0 = config2_x0(nb, 11)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    for N in (2, 3, 5, 17, 32, 33, 50, 63, 100, 127):
+        u = [twin.controller_solve(make_opts(N=N, sqp_iters=1, stages_per_lane=2, factor_scan=fs), x0, traj, 1,
+                                   twin.new_warm(nb, N), shape_id=sid)["u0"] for fs in (0, 1)]
+        np.testing.assert_allclose(u[1], u[0], rtol=0, atol=1e-15, err_msg=f"N={N}")

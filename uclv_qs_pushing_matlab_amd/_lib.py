@@ -12,7 +12,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 # QSP_LIB_PATH: developer override (A/B runs of differently compiled libraries)
 LIB_PATH = os.environ.get("QSP_LIB_PATH") or os.path.join(_PKG, "libqsp_nmpc.so")
 MAX_CTRL = 64
-ABI_VERSION = 2   # include/qsp_nmpc.h QSP_ABI_VERSION
+ABI_VERSION = 3   # include/qsp_nmpc.h QSP_ABI_VERSION
 
 _lib = None
 
@@ -32,7 +32,7 @@ class Options(C.Structure):
         ("res_stop", C.c_double),
         ("qp_tol_stat", C.c_double), ("qp_tol_eq", C.c_double),
         ("stage0_s_bound", C.c_int32), ("qp_stall_iters", C.c_int32), ("qp_stall_alpha", C.c_double),
-        ("qp_mu_max", C.c_double),
+        ("qp_mu_max", C.c_double), ("factor_scan", C.c_int32),
     ]
 
 

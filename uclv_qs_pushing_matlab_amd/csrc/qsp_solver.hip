@@ -40,9 +40,6 @@
 #ifndef QSP_MIN_WAVES
 #define QSP_MIN_WAVES 1
 #endif
-#ifndef QSP_S2_SCAN_FACTOR
-#define QSP_S2_SCAN_FACTOR 0
-#endif
 
 namespace qsp {
 
@@ -708,7 +705,7 @@ __device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const dou
 // Backward pass over the group (factorisation, or the corrector's difference recursion),
 // then forward pass writing the bounded components of the solution into LDS field `out`
 // (F_VA / F_VN).
-template <int S, bool FACTOR>
+template <int S, bool FACTOR, bool SCAN = false>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
                                               int out, double (&M)[S][16]) {
     double P[10], pv[4];
@@ -813,7 +810,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 st.kk[ls][1] += dkk[1];
             }
         }
-    } else if constexpr (S == 2 && FACTOR && QSP_S2_SCAN_FACTOR) {
+    } else if constexpr (S == 2 && FACTOR && SCAN) {
         // factorisation as a suffix scan of the lanes' value-function elements: lane j combines its
         // two stages' elements (slot 0's, then slot 1's; the terminal element where k = N, none past
         // it), Hillis-Steele levels give E_{2j:N}, the next lane's result E_{2j+2:N} gives slot 1's
@@ -1035,7 +1032,7 @@ enum QpExit : int { QP_EXIT_CONV = 0, QP_EXIT_CAP = 1, QP_EXIT_STALL = 2, QP_EXI
 // (1 - alpha), so each is its start value times prod(1 - alpha) (tracked, not recomputed:
 // r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)); the
 // test r * prod < tol is applied as prod < min(tol / r) over the three.
-template <int S>
+template <int S, bool SCAN = false>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], int& exit,
                       bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
@@ -1113,7 +1110,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls);
         double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
-        riccati_solve<S, true>(c, p, st, dx0, F_VA, M);
+        riccati_solve<S, true, SCAN>(c, p, st, dx0, F_VA, M);
         // affine directions: computed once, kept in registers through the corrector
         double at[S][6], al[S][6];
         double num = 1.0, den = 1.0;
@@ -1130,7 +1127,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         // ---- corrector
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, p, st, ls, at[ls], al[ls], smu);
-        riccati_solve<S, false>(c, p, st, dx0, F_VN, M);
+        riccati_solve<S, false, SCAN>(c, p, st, dx0, F_VN, M);
         double dt[S][6], dl[S][6];
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
@@ -1479,7 +1476,7 @@ __device__ __forceinline__ bool qp_outcome(const SolveArgs& A, const Ctx& c, con
     return failed;
 }
 
-template <int S, bool MERIT = false, bool LIN = false>
+template <int S, bool MERIT = false, bool LIN = false, bool SCAN = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -1591,7 +1588,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
     }
     int exit;
-    const int nit = qp_ipm<S>(c, p, st, dx0, exit, skip);
+    const int nit = qp_ipm<S, SCAN>(c, p, st, dx0, exit, skip);
     qp_rollout<S>(c, st, dx0);
     const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
     if (A.wnit && c.real && c.lig == 0) {
@@ -1666,7 +1663,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 // wave of the batch (no packing sort, no grid-wide boundary between SQP iterations).  The
 // per-iteration arithmetic is qp_step_kernel<S, false, true>'s (same helpers, same order), so
 // the results are bit-identical to the per-iteration launches (tests/test_gpu_fullsize.py).
-template <int S>
+template <int S, bool SCAN = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArgs A) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -1750,7 +1747,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
         for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
         const bool skip = stopped || !c.real;
         int exit;
-        const int nit = qp_ipm<S>(c, p, st, dx0, exit, skip);
+        const int nit = qp_ipm<S, SCAN>(c, p, st, dx0, exit, skip);
         qp_rollout<S>(c, st, dx0);
         const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
         qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real && !skip && !failed,
@@ -2311,29 +2308,30 @@ static hipError_t lds_attr_once(const void* kernel, int bytes, std::atomic<uint6
 
 // LIN: the SQP iteration's linearisation runs inside the QP kernel (nlp_mode 0); without
 // it the kernel reads the stage data the workspace holds (qsp_qp_solve).
-template <int S, bool LIN>
+// SCAN (S = 2 only, SolveParams::factor_scan): the factorisation runs as an associative scan
+template <int S, bool LIN, bool SCAN = false>
 static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN>, lds_bytes<S>(), attr);
+    const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN, SCAN>, lds_bytes<S>(), attr);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((qp_step_kernel<S, false, LIN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
+    hipLaunchKernelGGL((qp_step_kernel<S, false, LIN, SCAN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
     return hipGetLastError();
 }
 
-template <int S>
+template <int S, bool SCAN = false>
 static hipError_t launch_sqp_loop(const SolveArgs& a, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)sqp_loop_kernel<S>, lds_bytes<S>(), attr);
+    const hipError_t e = lds_attr_once((const void*)sqp_loop_kernel<S, SCAN>, lds_bytes<S>(), attr);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((sqp_loop_kernel<S>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a);
+    hipLaunchKernelGGL((sqp_loop_kernel<S, SCAN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a);
     return hipGetLastError();
 }
 
@@ -2351,7 +2349,10 @@ int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus) {
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
         case 1: return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
-        case 2: return lin ? launch_qp_step<2, true>(a, it, stream) : launch_qp_step<2, false>(a, it, stream);
+        case 2:
+            if (a.p.factor_scan)
+                return lin ? launch_qp_step<2, true, true>(a, it, stream) : launch_qp_step<2, false, true>(a, it, stream);
+            return lin ? launch_qp_step<2, true>(a, it, stream) : launch_qp_step<2, false>(a, it, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2439,7 +2440,9 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     }
     if (e == hipSuccess) e = mark();
     if (fused) {
-        if (e == hipSuccess) e = S == 1 ? launch_sqp_loop<1>(as, stream) : launch_sqp_loop<2>(as, stream);
+        if (e == hipSuccess)
+            e = S == 1 ? launch_sqp_loop<1>(as, stream)
+                       : (as.p.factor_scan ? launch_sqp_loop<2, true>(as, stream) : launch_sqp_loop<2>(as, stream));
         ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
     } else if (!two) {

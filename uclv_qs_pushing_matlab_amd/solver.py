@@ -24,7 +24,7 @@ class OcpSolver:
     def __init__(self, N=20, batch=1, Ts=0.05, sqp_iters=50, qp_iters=20, stages_per_lane=0, device=0,
                  cost_scale_Ts=True, mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10,
                  qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=True, qp_stall_iters=3, qp_stall_alpha=1e-3,
-                 qp_mu_max=1e100,
+                 qp_mu_max=1e100, factor_scan=False,
                  nlp_solver_type="SQP_RTI", tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
                  qp_solver_cond_N=None, timings=False):
         # qp_solver_cond_N (NMPC_controller.m:276) selects HPIPM's partial condensing, a different
@@ -47,6 +47,9 @@ class OcpSolver:
         o.stage0_s_bound = 1 if stage0_s_bound else 0
         o.qp_stall_iters, o.qp_stall_alpha = int(qp_stall_iters), float(qp_stall_alpha)
         o.qp_mu_max = float(qp_mu_max)
+        # two stages per lane (N + 1 > 32): the factorisation as an associative scan (faster, less
+        # accurate; include/qsp_nmpc.h)
+        o.factor_scan = 1 if factor_scan else 0
         if nlp_solver_type not in self.NLP_MODES:
             raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
         o.nlp_mode = self.NLP_MODES[nlp_solver_type]
