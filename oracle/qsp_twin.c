@@ -839,6 +839,32 @@ static void velem_combine(tw_velem *e, const tw_velem *f)
     }
 }
 
+/* developer check of the element arithmetic (scripts/ubench/velem_check.hip runs the same on the
+ * device): per case two stages (a, B, bb, Hx, Hu, gx, gu: 30 doubles each) and a terminal (We, g: 8);
+ * out = e0 (x) e1, then (x) the terminal element (We[0] > 0) or (x) e1 (x) e0 (We[0] <= 0): 2 x 44 doubles */
+void tw_velem_check(int32_t n, const double *in, double *out)
+{
+    for (int i = 0; i < n; ++i) {
+        const double *c = in + (size_t)i * 68;
+        tw_velem e, e1, t;
+        velem_stage(c, c + 6, c + 14, c + 18, c + 22, c + 24, c + 28, &e);
+        velem_stage(c + 30, c + 36, c + 44, c + 48, c + 52, c + 54, c + 58, &e1);
+        velem_combine(&e, &e1);
+        memcpy(out + (size_t)i * 88, &e, sizeof e);
+        const double g6[6] = {c[64], c[65], c[66], c[67], 0.0, 0.0};
+        if (c[60] > 0.0) {
+            velem_terminal(c + 60, g6, &t);
+        } else {   /* a general element on the right: the case's two stages combined in the other order */
+            tw_velem u;
+            velem_stage(c + 30, c + 36, c + 44, c + 48, c + 52, c + 54, c + 58, &t);
+            velem_stage(c, c + 6, c + 14, c + 18, c + 22, c + 24, c + 28, &u);
+            velem_combine(&t, &u);
+        }
+        velem_combine(&e, &t);
+        memcpy(out + (size_t)i * 88 + 44, &e, sizeof e);
+    }
+}
+
 /* the S = 2 factorisation: lane l combines its slots' elements, Hillis-Steele suffix levels over the
  * lanes, slot 1's suffix from the next lane's result; each slot then forms K, Rn, kk from its
  * successor's value function (ric_factor_step without the P update) */
