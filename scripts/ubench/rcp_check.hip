@@ -14,7 +14,7 @@ __global__ void rcp_kernel(const double* x, double* r, double* w, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         r[i] = qsp::rcp(x[i]);
-        w[i] = qsp::rcp_wide(x[i]);
+        w[i] = 1.0 / x[i];
     }
 }
 static uint64_t sm(uint64_t& s) {
@@ -40,7 +40,7 @@ int main() {
     hipLaunchKernelGGL(rcp_kernel, dim3(n / 256), dim3(256), 0, 0, dx, dr, dw, n);
     if (hipMemcpy(r.data(), dr, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
     if (hipMemcpy(w.data(), dw, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-    long bad = 0, badneg = 0, badw = 0, badw_normal = 0;
+    long bad = 0, badneg = 0, badw = 0, badw_normal = 0, bycls[3] = {0, 0, 0};
     long byexp[64] = {0}, cnt[64] = {0};
     for (int i = 0; i < n; ++i) {
         const double h = qsp::rcp_host(x[i]);
@@ -52,6 +52,7 @@ int main() {
             if (bad < 4) printf("x %.17g  device %.17g  host %.17g\n", x[i], r[i], h);
             ++bad;
             badneg += x[i] < 0;
+            bycls[(i % 8 == 1) ? 1 : ((i % 8 == 2) ? 2 : 0)]++;
             byexp[bucket]++;
         }
         if (memcmp(&h, &w[i], 8) != 0) {
@@ -63,6 +64,8 @@ int main() {
     printf("rcp by binary exponent (bucket of 32): ");
     for (int b = 0; b < 64; ++b)
         if (byexp[b]) printf("[%d,%d): %ld/%ld  ", b * 32 - 1024, b * 32 - 992, byexp[b], cnt[b]);
-    printf("\nrcp_wide: %ld differ (%ld where 1/x is a normal number)\n", badw, badw_normal);
+    printf("\nrcp differing by sample class: random mantissa %ld of %d, just above a power of two %ld of %d, "
+           "just below %ld of %d\n", bycls[0], n * 6 / 8, bycls[1], n / 8, bycls[2], n / 8);
+    printf("IEEE 1/x on the device: %ld differ from the host's rcp (%ld where 1/x is a normal number)\n", badw, badw_normal);
     return 0;
 }

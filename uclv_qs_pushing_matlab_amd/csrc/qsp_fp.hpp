@@ -32,18 +32,6 @@ __device__ __forceinline__ double rcp(double x) {
     e = __builtin_fma(-x, r, 1.0);
     return __builtin_fma(r, e, r);
 }
-// rcp for any exponent: the hardware reciprocal's estimate is not good enough for two Newton steps far
-// outside the binary32 exponent range (scripts/ubench/rcp_check.hip: about 1 % of arguments of random
-// exponent end one ulp off), so the mantissa is inverted and the exponent restored exactly.  The result
-// is the correctly rounded 1/x (the oracle's rcp) wherever that is a normal number.
-__device__ __forceinline__ double rcp_wide(double x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int e = __builtin_amdgcn_frexp_exp(x);
-    return __builtin_amdgcn_ldexp(rcp(__builtin_amdgcn_frexp_mant(x)), -e);
-#else
-    return rcp(x);
-#endif
-}
 // the host counterpart (developer tools; the oracle restates it in C)
 inline double rcp_host(double x) {
     double r = 1.0 / x;

@@ -459,9 +459,10 @@ __device__ __forceinline__ void velem_stage(const double a[6], const double B[8]
     const double F[16] = {1.0, 0.0, a[0], a[1], 0.0, 1.0, a[2], a[3], 0.0, 0.0, 1.0, a[4], 0.0, 0.0, 0.0, a[5]};
 #pragma unroll
     for (int q = 0; q < 16; ++q) e.A[q] = F[q];
-    // rcp_wide: barrier-modified Hessians and the pivots below reach far beyond the binary32 exponent
-    // range, where the hardware reciprocal's estimate is too coarse for rcp's two Newton steps
-    const double ih0 = rcp_wide(Hu[0]), ih1 = rcp_wide(Hu[1]);
+    // IEEE division, not rcp: the pivots below are often 1 + tiny, where rcp's refinement of the hardware
+    // estimate ends one ulp off the correctly rounded 1/x (scripts/ubench/rcp_check.hip); the division
+    // is the correctly rounded 1/x the oracle's rcp computes
+    const double ih0 = 1.0 / Hu[0], ih1 = 1.0 / Hu[1];
     const double v0 = ih0 * gu[0], v1 = ih1 * gu[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -496,7 +497,7 @@ __device__ __forceinline__ void velem_combine(VElem& e, const VElem& f) {
                       qfma(e.C[sidx(i, 1)], f.J[sidx(1, j)], qfma(e.C[sidx(i, 0)], f.J[sidx(0, j)], i == j ? 1.0 : 0.0))));
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const double piv = rcp_wide(T[c][c]);
+        const double piv = 1.0 / T[c][c];
         T[c][c] = 1.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) T[c][j] *= piv;
