@@ -102,7 +102,7 @@ typedef struct {
     int32_t factor_scan;      /* two stages per lane (S = 2: N + 1 > 32, e.g. N = 50) only.  0 (default): the
                                  Riccati factorisation walks the horizon stage by stage, as at S = 1 and in
                                  HPIPM.  1: it runs as an associative (parallel-in-time) scan of the stages'
-                                 value-function elements -- configs[4] 94k -> 116k solves/s on one MI355X, but
+                                 value-function elements -- configs[4] 94k -> 115k solves/s on one MI355X, but
                                  about two digits less accurate (u0 vs the extended-precision oracle: median
                                  8e-11 instead of 2e-12 after 5 SQP iterations), which the fixed-K SQP's
                                  rounding sensitivity turns into more lanes off the reference */
