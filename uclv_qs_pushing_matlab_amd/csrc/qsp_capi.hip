@@ -77,6 +77,7 @@ struct qsp_solver {
     SqpStreams split;
     int parts_req = 0;
     int fused_req = -1;            // QSP_FUSED_LOOP (-1: auto)
+    bool nopack = false;           // QSP_PACKING=0: instances in lane order (developer A/B of the wave packing)
     int cus = 256;                 // compute units of the device (hipDeviceProp multiProcessorCount)
 };
 
@@ -222,7 +223,7 @@ static SolveArgs make_args(qsp_solver* s) {
     a.wdone = s->wdone.as<int32_t>();
     a.wres = s->wres.as<double>();
     a.wqp = s->wqp.as<double>();
-    a.wperm = s->wperm.as<int32_t>();
+    a.wperm = s->nopack ? nullptr : s->wperm.as<int32_t>();
     if (s->poison) a.flags |= QSP_FLAG_POISON;
     a.wnit = s->wnit.as<int32_t>();
     a.whist = s->whist.as<int32_t>();
@@ -438,6 +439,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     // debug: every workspace byte starts as a NaN pattern, so a kernel that reads a word it
     // never wrote shows up as NaN (tests/test_gpu_errors.py)
     if (const char* fl = std::getenv("QSP_FUSED_LOOP")) s->fused_req = (fl[0] == '1') ? 1 : (fl[0] == '0' ? 0 : -1);
+    if (const char* pk = std::getenv("QSP_PACKING")) s->nopack = pk[0] == '0';
     const char* pz = std::getenv("QSP_DEBUG_POISON");
     s->poison = pz && pz[0] == '1';
     if (s->poison) {
