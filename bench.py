@@ -537,9 +537,8 @@ def main():
                          "-2.2 %% here, but 2.3x slower at B = 4 096 where every SQP iteration waits for its slowest "
                          "wave; DESIGN.md section 1)")
     ap.add_argument("--stages-per-lane", type=int, default=0)
-    ap.add_argument("--factor-scan", type=int, default=None,
-                    help="two stages per lane: leading IPM iterations whose factorisation runs as an associative scan "
-                         "(qsp_options.factor_scan; 255 = all; default: the library's)")
+    ap.add_argument("--factor-scan", action="store_true",
+                    help="two stages per lane: the factorisation as an associative scan (qsp_options.factor_scan)")
     ap.add_argument("--stream-parts", type=int, default=0, choices=(0, 1, 2),
                     help="SQP loop in 1 or 2 lane parts on their own HIP streams (0 = the library's auto choice)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -604,8 +603,7 @@ def main():
     Bl = hi - lo
 
     solver = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=args.qp_iters, stages_per_lane=args.stages_per_lane,
-                       device=gpu, nlp_solver_type=args.nlp,
-                       **({} if args.factor_scan is None else {"factor_scan": args.factor_scan}))
+                       device=gpu, nlp_solver_type=args.nlp, factor_scan=args.factor_scan)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
     solver.set_stream_parts(args.stream_parts)
@@ -724,7 +722,7 @@ def main():
                    "global_batch": total, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
                    "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
-                              "stream_parts": parts, "factor_scan": int(solver.opts.factor_scan) if S_layout == 2 else 0},
+                              "stream_parts": parts, "factor_scan": bool(args.factor_scan and S_layout == 2)},
                    "parallelism": f"dp{world} (contiguous lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),

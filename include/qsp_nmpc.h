@@ -39,7 +39,6 @@ extern "C" {
 #define QSP_NY_E 4
 #define QSP_NH 3          /* h = [s; u_n; u_t]      (NMPC_controller.m:237) */
 #define QSP_MAX_CTRL 64   /* spline control points per shape */
-#define QSP_FACTOR_SCAN_ALL 255 /* qsp_options.factor_scan: every IPM iteration (qp_iters <= 255) */
 #define QSP_ABI_VERSION 3 /* 2: struct_size fields, qp_mu_max, qsp_get_qp_stalled, QP-failure exits;
                              3: qsp_options.factor_scan */
 
@@ -100,17 +99,13 @@ typedef struct {
                                  iterate) instead of overflowing to NaN; default 1e100 (mu starts at mu0 = 1:
                                  an overflow guard -- QPs whose mu grows large but finite end at the stall
                                  exit, from which the SQP recovers; measured on the bench workload) */
-    int32_t factor_scan;      /* two stages per lane (S = 2: N + 1 > 32, e.g. N = 50) only: the number of leading
-                                 interior-point iterations of every QP whose Riccati factorisation runs as an
-                                 associative (parallel-in-time) scan of the stages' value-function elements; the
-                                 later iterations walk the horizon stage by stage, as at S = 1 and in HPIPM.
-                                 0 (default): the walk throughout.  QSP_FACTOR_SCAN_ALL: the scan throughout --
-                                 configs[4] 94k -> 115k solves/s on one MI355X, but about two digits less
-                                 accurate (u0 vs the extended-precision oracle: median 8e-11 instead of 2e-12
-                                 after 5 SQP iterations), which the fixed-K SQP's rounding sensitivity turns into
-                                 more lanes off the reference.  A few leading iterations (far from the solution,
-                                 where the Newton directions need no last digits) keep the walk's accuracy
-                                  */
+    int32_t factor_scan;      /* two stages per lane (S = 2: N + 1 > 32, e.g. N = 50) only.  0 (default): the
+                                 Riccati factorisation walks the horizon stage by stage, as at S = 1 and in
+                                 HPIPM.  1: it runs as an associative (parallel-in-time) scan of the stages'
+                                 value-function elements -- configs[4] 94k -> 115k solves/s on one MI355X, but
+                                 about two digits less accurate (u0 vs the extended-precision oracle: median
+                                 8e-11 instead of 2e-12 after 5 SQP iterations), which the fixed-K SQP's
+                                 rounding sensitivity turns into more lanes off the reference */
 } qsp_options;
 
 /* One slider shape: object_selection.m:3-42 + PusherSliderModel.m:84-132. */

@@ -12,7 +12,7 @@
  *        nlp_solver_max_iter (30 for SQP, 1 for SQP_RTI), nlp_solver_tol_stat/eq/ineq/comp (1e-6),
  *        qp_solver_iter_max (50 for SQP, 20 for SQP_RTI), globalization_alpha_min (0.05), globalization_alpha_reduction
  *        (0.7), eps_sufficient_descent (1e-4), stage0_s_bound (1), stages_per_lane (0 = auto),
- *        factor_scan (leading IPM iterations factorised by the S = 2 scan; 255 = all: faster, less accurate),
+ *        factor_scan (0; 1 = the S = 2 factorisation as an associative scan: faster, less accurate),
  *        device (0), qp_solver_cond_N (1..N; validated only, see below)  -- NMPC_controller.m:270-300
  *   d = qsp_nmpc_mex('dims', h)                          % [N B]
  *   qsp_nmpc_mex('shape_ply', h, {ply, flip, mu_sg, mu_sp, m, tau_max, xwidth; ...}, shape_id)

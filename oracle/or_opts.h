@@ -56,8 +56,8 @@ typedef struct {
      * of the model from the others.  0: off. */
     double model_probe;
     int32_t probe_seed;
-    int32_t factor_scan; /* twin only: at S = 2 the factorisation of the first factor_scan IPM iterations of
-                            every QP as the device's associative scan, then the walk (qsp_options.factor_scan) */
+    int32_t factor_scan; /* twin only: at S = 2 the factorisation as the device's associative scan
+                            (qsp_options.factor_scan) instead of the walk */
 } or_opts;
 
 #endif

@@ -83,7 +83,7 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
     o.qp_stall_alpha, o.qp_stall_iters = qp_stall_alpha, int(qp_stall_iters)
     o.qp_mu_max, o.stages_per_lane = qp_mu_max, int(stages_per_lane)
     o.model_probe, o.probe_seed = float(model_probe), int(probe_seed)
-    o.factor_scan = 255 if factor_scan is True else int(factor_scan)   # True: every IPM iteration
+    o.factor_scan = int(factor_scan)
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W

@@ -381,7 +381,7 @@ static void make_par(tw_par *p, const or_opts *o)
     p->qp_iters = o->qp_iters;
     p->qp_stall_iters = o->qp_stall_iters;
     p->s0_bound = o->stage0_s_bound ? 1 : 0;
-    p->factor_scan = o->factor_scan > 0 ? o->factor_scan : 0;
+    p->factor_scan = o->factor_scan ? 1 : 0;
     p->Ts = o->Ts;
     p->tau = o->tau;
     memcpy(p->W, o->W, sizeof p->W);
@@ -923,7 +923,7 @@ static void factor_scan_s2(const tw_par *p, tw_stage *st, const double *hx3, dou
 
 /* riccati_solve: factor (predictor) or the corrector's difference recursion, then the forward pass
  * writing the bounded solution components into VA (factor) / VN (corrector) */
-static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], int factor, int it)
+static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], int factor)
 {
     const int N = p->N, S = p->S;
     double P[10], pv[4];
@@ -964,7 +964,7 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
         }
     } else if (S == 2 && !factor) {
         delta_scan_s2(p, st, gx3, gu);
-    } else if (S == 2 && factor && it < p->factor_scan) {   /* the scan for the leading IPM iterations */
+    } else if (S == 2 && factor && p->factor_scan) {
         factor_scan_s2(p, st, hx3, hu, gx3, gu);
     } else {
         if (factor) {
@@ -1090,7 +1090,7 @@ static int qp_ipm(const tw_par *p, tw_stage *st, const double dx0[4], int *exit,
         nit++;
         /* predictor */
         for (int k = 0; k < L * S; ++k) barrier_terms(p, st + k, k);
-        riccati_solve(p, st, dx0, 1, it);
+        riccati_solve(p, st, dx0, 1);
         for (int l = 0; l < L; ++l) {
             num[l] = 1.0;
             den[l] = 1.0;
@@ -1109,7 +1109,7 @@ static int qp_ipm(const tw_par *p, tw_stage *st, const double dx0[4], int *exit,
         const double smu = sg * mu;
         /* corrector */
         for (int k = 0; k < L * S; ++k) corrector_terms(p, st + k, k, smu);
-        riccati_solve(p, st, dx0, 0, it);
+        riccati_solve(p, st, dx0, 0);
         for (int l = 0; l < L; ++l) {
             num[l] = 1.0;
             den[l] = p->frac;

@@ -243,5 +243,5 @@ def test_factor_scan_s2_matches_walk_at_one_iteration(twin):
     traj = straight_traj()
     for N in (2, 3, 5, 17, 32, 33, 50, 63, 100, 127):
         u = [twin.controller_solve(make_opts(N=N, sqp_iters=1, stages_per_lane=2, factor_scan=fs), x0, traj, 1,
-                                   twin.new_warm(nb, N), shape_id=sid)["u0"] for fs in (0, True)]
+                                   twin.new_warm(nb, N), shape_id=sid)["u0"] for fs in (0, 1)]
         np.testing.assert_allclose(u[1], u[0], rtol=0, atol=1e-15, err_msg=f"N={N}")

@@ -131,7 +131,7 @@ static void fill_params(qsp_solver* s) {
     p.qp_tol_stat = s->o.qp_tol_stat;
     p.qp_tol_eq = s->o.qp_tol_eq;
     p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
-    p.factor_scan = s->o.factor_scan;
+    p.factor_scan = s->o.factor_scan ? 1 : 0;
     p.qp_stall_iters = s->o.qp_stall_iters;
     p.qp_stall_alpha = s->o.qp_stall_alpha;
     p.qp_mu_max = s->o.qp_mu_max;
@@ -361,8 +361,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (o->sqp_iters < 1 || o->qp_iters < 1) return fail(QSP_ERR_ARG, "qsp_create: iteration counts must be >= 1");
     if (o->qp_iters > 255) return fail(QSP_ERR_ARG, "qsp_create: qp_iters must be <= 255");
     if (o->qp_stall_iters < 0) return fail(QSP_ERR_ARG, "qsp_create: qp_stall_iters must be >= 0");
-    if (o->factor_scan < 0 || o->factor_scan > QSP_FACTOR_SCAN_ALL)
-        return fail(QSP_ERR_ARG, "qsp_create: factor_scan must be in 0..QSP_FACTOR_SCAN_ALL");
+    if (o->factor_scan != 0 && o->factor_scan != 1) return fail(QSP_ERR_ARG, "qsp_create: factor_scan must be 0 or 1");
     if (!(o->qp_tol_stat > 0.0) || !(o->qp_tol_eq > 0.0) || !(o->mu_stop > 0.0) || !(o->res_stop > 0.0))
         return fail(QSP_ERR_ARG, "qsp_create: QP stop tolerances must be > 0");
     if (!(o->Ts > 0.0)) return fail(QSP_ERR_ARG, "qsp_create: Ts must be > 0");

@@ -708,12 +708,9 @@ __device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const dou
 // Backward pass over the group (factorisation, or the corrector's difference recursion),
 // then forward pass writing the bounded components of the solution into LDS field `out`
 // (F_VA / F_VN).
-// SCAN (S = 2 factorisation, qsp_options.factor_scan): SCAN_NONE the walk; SCAN_ALL the associative
-// scan; SCAN_LEAD the scan while scan_now (the leading IPM iterations), then the walk
-enum ScanMode : int { SCAN_NONE = 0, SCAN_ALL = 1, SCAN_LEAD = 2 };
-template <int S, bool FACTOR, int SCAN = SCAN_NONE>
+template <int S, bool FACTOR, bool SCAN = false>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
-                                              int out, double (&M)[S][16], bool scan_now = false) {
+                                              int out, double (&M)[S][16]) {
     double P[10], pv[4];
 #pragma unroll
     for (int i = 0; i < 10; ++i) P[i] = 0.0;
@@ -747,51 +744,6 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             gu[ls][1] = st.hg(ls, 5);
         }
     }
-    // the backward walk (factorisation or the corrector's difference recursion) along the lanes
-    auto walk_back = [&]() {
-        for (int j = c.L - 1; j >= 0; --j) {
-            // Lanes above j already hold their final factors and sit the step out (exec
-            // mask); lanes below j compute a throw-away step that their own turn overwrites.
-            // Writing the factors in place this way needs no per-step selects.
-            // The hand-over runs inside the same region: lane j-1 (active) reads lane j (active).
-            if (c.lig <= j) {
-                double Pc[10], pvc[4];
-#pragma unroll
-                for (int i = 0; i < 10; ++i) Pc[i] = P[i];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) pvc[i] = pv[i];
-#pragma unroll
-                for (int ls = S - 1; ls >= 0; --ls) {
-                    if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
-                    if (FACTOR) {
-                        const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], gx3[ls]};
-                        const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[ls]};
-                        ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, hu[ls], gx, gu[ls], Pc, pvc, st.K[ls],
-                                        st.Rn[ls], st.kk[ls], j > 0 || ls > 0);
-                    } else {
-                        double dkk[2];
-                        ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvc, dkk);
-                        // in place only on the lane's own turn (a throw-away step must not accumulate)
-                        if (c.lig == j) {
-                            st.kk[ls][0] += dkk[0];
-                            st.kk[ls][1] += dkk[1];
-                        }
-                    }
-                }
-                // hand-over to lane j-1 (none after step 0: lane 0 reads a disabled lane there).  The
-                // first step of a last lane without a stage (lsN == 0) leaves P at the terminal
-                // diag(We) every lane already holds, so only p moves then.
-                if (j > 0) {
-                    if (FACTOR && !(j == c.L - 1 && lsN == 0)) {
-#pragma unroll
-                        for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i], Pc[i]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
-                }
-            }
-        }
-    };
     if constexpr (S == 1 && !FACTOR) {
         // corrector difference walk in closed-loop form: dp_k = e_k + (A + B K)' dp_{k+1} with
         // e = dg_x + K' dg_u (ric_delta_step with dr = dg_u + B' dp substituted), a 4x4 map per
@@ -861,64 +813,100 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 st.kk[ls][1] += dkk[1];
             }
         }
-    } else if constexpr (S == 2 && FACTOR && SCAN != SCAN_NONE) {
-        if (SCAN == SCAN_ALL || scan_now) {
-            // factorisation as a suffix scan of the lanes' value-function elements: lane j combines its
-            // two stages' elements (slot 0's, then slot 1's; the terminal element where k = N, none past
-            // it), Hillis-Steele levels give E_{2j:N}, the next lane's result E_{2j+2:N} gives slot 1's
-            // E_{2j+1:N}; then each slot forms K, Rn, kk from its successor's value function
-            const int k0 = 2 * c.lig, k1 = k0 + 1;
-            VElem e, e1;
-            {
-                const double Hx0[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
-                const double gxa[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
-                if (k0 < c.N) velem_stage(st.a[0], st.B[0], st.bb[0], Hx0, hu[0], gxa, gu[0], e);
-                else velem_terminal(p.We, st.g[0], e);
-                const double Hx1[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
-                const double gxb[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
-                if (k1 < c.N) velem_stage(st.a[1], st.B[1], st.bb[1], Hx1, hu[1], gxb, gu[1], e1);
-                else velem_terminal(p.We, st.g[1], e1);
-                if (k1 <= c.N) {
-                    VElem t = e1;
-                    velem_combine(e, t);
-                }
+    } else if constexpr (S == 2 && FACTOR && SCAN) {
+        // factorisation as a suffix scan of the lanes' value-function elements: lane j combines its
+        // two stages' elements (slot 0's, then slot 1's; the terminal element where k = N, none past
+        // it), Hillis-Steele levels give E_{2j:N}, the next lane's result E_{2j+2:N} gives slot 1's
+        // E_{2j+1:N}; then each slot forms K, Rn, kk from its successor's value function
+        const int k0 = 2 * c.lig, k1 = k0 + 1;
+        VElem e, e1;
+        {
+            const double Hx0[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
+            const double gxa[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
+            if (k0 < c.N) velem_stage(st.a[0], st.B[0], st.bb[0], Hx0, hu[0], gxa, gu[0], e);
+            else velem_terminal(p.We, st.g[0], e);
+            const double Hx1[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
+            const double gxb[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
+            if (k1 < c.N) velem_stage(st.a[1], st.B[1], st.bb[1], Hx1, hu[1], gxb, gu[1], e1);
+            else velem_terminal(p.We, st.g[1], e1);
+            if (k1 <= c.N) {
+                VElem t = e1;
+                velem_combine(e, t);
             }
-            for (int off = 1; off < c.L; off <<= 1) {
-                const bool take = c.lig + off < c.L;
-                VElem f;
-                velem_read(e, take ? c.lane + off : c.lane, f);
-                if (take) velem_combine(e, f);
-            }
-            {
-                VElem f;
-                velem_read(e, c.lig + 1 < c.L ? c.lane + 1 : c.lane, f);
-                if (k1 < c.N) {
-                    velem_combine(e1, f);
-                    double Pn[10], pn[4];
-#pragma unroll
-                    for (int q = 0; q < 10; ++q) Pn[q] = f.J[q];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) pn[q] = -f.eta[q];
-                    const double gx[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
-                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
-                    ric_factor_step(st.a[1], st.B[1], st.bb[1], Hx, hu[1], gx, gu[1], Pn, pn, st.K[1], st.Rn[1], st.kk[1], false);
-                }
-                if (k0 < c.N) {
-                    double Pn[10], pn[4];
-#pragma unroll
-                    for (int q = 0; q < 10; ++q) Pn[q] = e1.J[q];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) pn[q] = -e1.eta[q];
-                    const double gx[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
-                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
-                    ric_factor_step(st.a[0], st.B[0], st.bb[0], Hx, hu[0], gx, gu[0], Pn, pn, st.K[0], st.Rn[0], st.kk[0], false);
-                }
-            }
-        } else {
-            walk_back();
         }
-    } else {
-        walk_back();
+        for (int off = 1; off < c.L; off <<= 1) {
+            const bool take = c.lig + off < c.L;
+            VElem f;
+            velem_read(e, take ? c.lane + off : c.lane, f);
+            if (take) velem_combine(e, f);
+        }
+        {
+            VElem f;
+            velem_read(e, c.lig + 1 < c.L ? c.lane + 1 : c.lane, f);
+            if (k1 < c.N) {
+                velem_combine(e1, f);
+                double Pn[10], pn[4];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) Pn[q] = f.J[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pn[q] = -f.eta[q];
+                const double gx[4] = {st.g[1][0], st.g[1][1], st.g[1][2], gx3[1]};
+                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[1]};
+                ric_factor_step(st.a[1], st.B[1], st.bb[1], Hx, hu[1], gx, gu[1], Pn, pn, st.K[1], st.Rn[1], st.kk[1], false);
+            }
+            if (k0 < c.N) {
+                double Pn[10], pn[4];
+#pragma unroll
+                for (int q = 0; q < 10; ++q) Pn[q] = e1.J[q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pn[q] = -e1.eta[q];
+                const double gx[4] = {st.g[0][0], st.g[0][1], st.g[0][2], gx3[0]};
+                const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[0]};
+                ric_factor_step(st.a[0], st.B[0], st.bb[0], Hx, hu[0], gx, gu[0], Pn, pn, st.K[0], st.Rn[0], st.kk[0], false);
+            }
+        }
+    } else
+    for (int j = c.L - 1; j >= 0; --j) {
+        // Lanes above j already hold their final factors and sit the step out (exec
+        // mask); lanes below j compute a throw-away step that their own turn overwrites.
+        // Writing the factors in place this way needs no per-step selects.
+        // The hand-over runs inside the same region: lane j-1 (active) reads lane j (active).
+        if (c.lig <= j) {
+            double Pc[10], pvc[4];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) Pc[i] = P[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pvc[i] = pv[i];
+#pragma unroll
+            for (int ls = S - 1; ls >= 0; --ls) {
+                if (j == c.L - 1 && ls >= lsN) continue;     // terminal / padding slots of the last lane
+                if (FACTOR) {
+                    const double gx[4] = {st.g[ls][0], st.g[ls][1], st.g[ls][2], gx3[ls]};
+                    const double Hx[4] = {p.tau * p.W[0], p.tau * p.W[1], p.tau * p.W[2], hx3[ls]};
+                    ric_factor_step(st.a[ls], st.B[ls], st.bb[ls], Hx, hu[ls], gx, gu[ls], Pc, pvc, st.K[ls],
+                                    st.Rn[ls], st.kk[ls], j > 0 || ls > 0);
+                } else {
+                    double dkk[2];
+                    ric_delta_step(st.a[ls], st.B[ls], gx3[ls], gu[ls], st.K[ls], st.Rn[ls], pvc, dkk);
+                    // in place only on the lane's own turn (a throw-away step must not accumulate)
+                    if (c.lig == j) {
+                        st.kk[ls][0] += dkk[0];
+                        st.kk[ls][1] += dkk[1];
+                    }
+                }
+            }
+            // hand-over to lane j-1 (none after step 0: lane 0 reads a disabled lane there).  The
+            // first step of a last lane without a stage (lsN == 0) leaves P at the terminal
+            // diag(We) every lane already holds, so only p moves then.
+            if (j > 0) {
+                if (FACTOR && !(j == c.L - 1 && lsN == 0)) {
+#pragma unroll
+                    for (int i = 0; i < 10; ++i) P[i] = wave_from_next(P[i], Pc[i]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
+            }
+        }
     }
     if constexpr (S == 1) {
         // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
@@ -1047,7 +1035,7 @@ enum QpExit : int { QP_EXIT_CONV = 0, QP_EXIT_CAP = 1, QP_EXIT_STALL = 2, QP_EXI
 // (1 - alpha), so each is its start value times prod(1 - alpha) (tracked, not recomputed:
 // r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)); the
 // test r * prod < tol is applied as prod < min(tol / r) over the three.
-template <int S, int SCAN = SCAN_NONE>
+template <int S, bool SCAN = false>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], int& exit,
                       bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
@@ -1125,7 +1113,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls);
         double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
-        riccati_solve<S, true, SCAN>(c, p, st, dx0, F_VA, M, it < p.factor_scan);
+        riccati_solve<S, true, SCAN>(c, p, st, dx0, F_VA, M);
         // affine directions: computed once, kept in registers through the corrector
         double at[S][6], al[S][6];
         double num = 1.0, den = 1.0;
@@ -1491,7 +1479,7 @@ __device__ __forceinline__ bool qp_outcome(const SolveArgs& A, const Ctx& c, con
     return failed;
 }
 
-template <int S, bool MERIT = false, bool LIN = false, int SCAN = SCAN_NONE>
+template <int S, bool MERIT = false, bool LIN = false, bool SCAN = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -1678,7 +1666,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 // wave of the batch (no packing sort, no grid-wide boundary between SQP iterations).  The
 // per-iteration arithmetic is qp_step_kernel<S, false, true>'s (same helpers, same order), so
 // the results are bit-identical to the per-iteration launches (tests/test_gpu_fullsize.py).
-template <int S, int SCAN = SCAN_NONE>
+template <int S, bool SCAN = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArgs A) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -2324,7 +2312,7 @@ static hipError_t lds_attr_once(const void* kernel, int bytes, std::atomic<uint6
 // LIN: the SQP iteration's linearisation runs inside the QP kernel (nlp_mode 0); without
 // it the kernel reads the stage data the workspace holds (qsp_qp_solve).
 // SCAN (S = 2 only, SolveParams::factor_scan): the factorisation runs as an associative scan
-template <int S, bool LIN, int SCAN = SCAN_NONE>
+template <int S, bool LIN, bool SCAN = false>
 static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
@@ -2337,7 +2325,7 @@ static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream)
     return hipGetLastError();
 }
 
-template <int S, int SCAN = SCAN_NONE>
+template <int S, bool SCAN = false>
 static hipError_t launch_sqp_loop(const SolveArgs& a, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
@@ -2361,23 +2349,13 @@ int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus) {
     return (nlp_mode == 0 && (S == 1 || S == 2) && waves <= 4L * cus) ? 1 : 0;
 }
 
-// factor_scan = the number of leading IPM iterations of every QP whose factorisation runs as the scan
-static int scan_mode(const SolveParams& p) {
-    return p.factor_scan <= 0 ? SCAN_NONE : (p.factor_scan >= p.qp_iters ? SCAN_ALL : SCAN_LEAD);
-}
-
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
         case 1: return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
         case 2:
-            switch (scan_mode(a.p)) {
-                case SCAN_ALL:
-                    return lin ? launch_qp_step<2, true, SCAN_ALL>(a, it, stream) : launch_qp_step<2, false, SCAN_ALL>(a, it, stream);
-                case SCAN_LEAD:
-                    return lin ? launch_qp_step<2, true, SCAN_LEAD>(a, it, stream) : launch_qp_step<2, false, SCAN_LEAD>(a, it, stream);
-                default:
-                    return lin ? launch_qp_step<2, true>(a, it, stream) : launch_qp_step<2, false>(a, it, stream);
-            }
+            if (a.p.factor_scan)
+                return lin ? launch_qp_step<2, true, true>(a, it, stream) : launch_qp_step<2, false, true>(a, it, stream);
+            return lin ? launch_qp_step<2, true>(a, it, stream) : launch_qp_step<2, false>(a, it, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2467,9 +2445,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (fused) {
         if (e == hipSuccess)
             e = S == 1 ? launch_sqp_loop<1>(as, stream)
-                       : (scan_mode(as.p) == SCAN_ALL ? launch_sqp_loop<2, SCAN_ALL>(as, stream)
-                          : (scan_mode(as.p) == SCAN_LEAD ? launch_sqp_loop<2, SCAN_LEAD>(as, stream)
-                                                          : launch_sqp_loop<2>(as, stream)));
+                       : (as.p.factor_scan ? launch_sqp_loop<2, true>(as, stream) : launch_sqp_loop<2>(as, stream));
         ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
     } else if (!two) {

@@ -16,9 +16,6 @@ from . import _lib
 from ._lib import check, f64, i32, ptr
 
 
-FACTOR_SCAN_ALL = 255   # include/qsp_nmpc.h QSP_FACTOR_SCAN_ALL
-
-
 class OcpSolver:
     # nlp_solver_type (NMPC_controller.m:271): 'SQP_RTI' = fixed-K full steps (the BASELINE
     # metric), 'SQP' = merit backtracking + KKT tolerances (the reference's own options)
@@ -50,9 +47,9 @@ class OcpSolver:
         o.stage0_s_bound = 1 if stage0_s_bound else 0
         o.qp_stall_iters, o.qp_stall_alpha = int(qp_stall_iters), float(qp_stall_alpha)
         o.qp_mu_max = float(qp_mu_max)
-        # two stages per lane (N + 1 > 32): the factorisation of the first `factor_scan` IPM iterations of
-        # every QP as an associative scan (True: all of them -- faster, less accurate; include/qsp_nmpc.h)
-        o.factor_scan = FACTOR_SCAN_ALL if factor_scan is True else int(factor_scan)
+        # two stages per lane (N + 1 > 32): the factorisation as an associative scan (faster, less
+        # accurate; include/qsp_nmpc.h)
+        o.factor_scan = 1 if factor_scan else 0
         if nlp_solver_type not in self.NLP_MODES:
             raise ValueError(f"nlp_solver_type must be one of {tuple(self.NLP_MODES)}")
         o.nlp_mode = self.NLP_MODES[nlp_solver_type]
