@@ -79,6 +79,30 @@ def test_two_stream_parts_bit_identical(nlp_mode, B, K):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("S", [1, 2])
+def test_wave_packing_off_bit_identical(monkeypatch, S):
+    """The wave packing (sort_by_iters_kernel) only reorders independent instances: with it off
+    (QSP_PACKING=0, the developer switch behind profiles/r05/traffic_ab.txt) every lane gets the same
+    bits, in both lane layouts."""
+    from bench import make_inputs
+    from uclv_qs_pushing_matlab_amd.objects import make_shape
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    N, B, K = 20, 8192, 8
+    x0, yref, yref_e, sid, traj = make_inputs(B, N, 20250303 + 5)
+    out = {}
+    for pk in ("1", "0"):
+        monkeypatch.setenv("QSP_PACKING", pk)
+        s = OcpSolver(N=N, batch=B, sqp_iters=K, stages_per_lane=S)
+        s.set_shapes([make_shape(n) for n in NAMES])
+        s.set_reference_trajectory(traj)
+        s.set_shape_ids(sid)
+        u = s.controller_solve(x0, 1)
+        out[pk] = [u] + [s.get(f) for f in ("x", "u", "pi", "status", "qp_iter")]
+        s.close()
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_stream_parts_auto_and_errors():
     """auto: one part below one fill of the 2 048 wave slots (B = 4 096: 1 366 waves of three
     instances), two from there on (B = 8 192); only 0, 1, 2 are accepted."""
