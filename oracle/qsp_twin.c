@@ -356,7 +356,7 @@ typedef struct {
 
 /* the solve parameters the kernels read (SolveParams): the options plus the QP-level overrides */
 typedef struct {
-    int N, S, L, nlp_mode, sqp_iters, qp_iters, qp_stall_iters, s0_bound, factor_scan;
+    int N, S, L, nlp_mode, sqp_iters, qp_iters, qp_stall_iters, s0_bound, factor_scan, mfma_walk;
     double Ts, tau, W[6], We[4], lh[3], uh[3];
     double mu0, t_min, frac, sigma_min, mu_stop, res_stop, qp_tol_stat, qp_tol_eq, qp_stall_alpha, qp_mu_max;
     double tol_stat, tol_eq, tol_ineq, tol_comp, ls_alpha_min, ls_alpha_red, ls_eps;
@@ -382,6 +382,10 @@ static void make_par(tw_par *p, const or_opts *o)
     p->qp_stall_iters = o->qp_stall_iters;
     p->s0_bound = o->stage0_s_bound ? 1 : 0;
     p->factor_scan = o->factor_scan ? 1 : 0;
+    /* the kernels factorise on the matrix cores at one stage per lane and 15 <= N <= 31 (mfw_use),
+     * unless the library's developer switch QSP_MFMA_WALK=0 selects the lane walk there too */
+    const char *mw = getenv("QSP_MFMA_WALK");
+    p->mfma_walk = p->S == 1 && p->N >= 15 && p->N <= 31 && !(mw && mw[0] == '0');
     p->Ts = o->Ts;
     p->tau = o->tau;
     memcpy(p->W, o->W, sizeof p->W);
@@ -923,6 +927,92 @@ static void factor_scan_s2(const tw_par *p, tw_stage *st, const double *hx3, dou
 
 /* riccati_solve: factor (predictor) or the corrector's difference recursion, then the forward pass
  * writing the bounded solution components into VA (factor) / VN (corrector) */
+/* mfma4: D = X'Y + C for 4x4 blocks held row-major (X read transposed, as the kernel's A operand);
+ * every element is one fused multiply-add chain over k = 0..3 starting from C, the order of
+ * v_mfma_f64_4x4x4_4b_f64 (scripts/ubench/mfma_f64_round.hip: 1 920 000 of 1 920 000 elements) */
+static void mfma4(const double X[16], const double Y[16], const double C[16], double D[16])
+{
+    double T[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double d = C[4 * i + j];
+            for (int k = 0; k < 4; ++k) d = fma(X[4 * k + i], Y[4 * k + j], d);
+            T[4 * i + j] = d;
+        }
+    memcpy(D, T, sizeof T);
+}
+
+/* factor_walk_mfma (qsp_solver.hip): the factorisation of one stage per lane on the matrix cores.
+ * The value function is a full symmetric 4x4 P and p replicated across the columns; a step is
+ * T1 = P'A, T2 = P'[B | b | 0] + [0 | 0 | p | 0], Q = A'T1 + Hx, Y = G'T1, Z = G'T2 + [Hu | gu],
+ * q = A'pp + gx, K = (-adj R~)'S~ / det, P = Y'K + Q (upper triangle; lower = K'Y + Q' elementwise,
+ * its exact transpose), p = K'[r~] + q; the stage keeps K and forms -R~^-1 and kk from Z's R~, r~. */
+static void factor_walk_mfma(const tw_par *p, tw_stage *st, const double *hx3, double (*hu)[2], const double *gx3,
+                             double (*gu)[2])
+{
+    const int N = p->N;
+    static const double zero[16] = {0};
+    double P[16] = {0}, pv[16];
+    for (int i = 0; i < 4; ++i) P[5 * i] = p->We[i];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) pv[4 * r + c] = st[N].g[r];
+    for (int k = N - 1; k >= 0; --k) {
+        tw_stage *s = st + k;
+        const double *a = s->a;
+        const double Am[16] = {1.0, 0.0, a[0], a[1], 0.0, 1.0, a[2], a[3], 0.0, 0.0, 1.0, a[4], 0.0, 0.0, 0.0, a[5]};
+        const double gx[4] = {s->g[0], s->g[1], s->g[2], gx3[k]};
+        double G2[16], CH[16] = {0}, CZ[16] = {0}, GQ[16], C2[16] = {0}, PP[16];
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) {
+                G2[4 * r + c] = c < 2 ? s->B[2 * r + c] : (c == 2 ? s->bb[r] : 0.0);
+                GQ[4 * r + c] = gx[r];
+            }
+        CH[0] = p->tau * p->W[0];
+        CH[5] = p->tau * p->W[1];
+        CH[10] = p->tau * p->W[2];
+        CH[15] = hx3[k];
+        CZ[0] = hu[k][0];
+        CZ[5] = hu[k][1];
+        CZ[2] = gu[k][0];
+        CZ[6] = gu[k][1];
+        for (int r = 0; r < 4; ++r) C2[4 * r + 2] = pv[4 * r + 2];
+        double T1[16], T2[16], Q[16], Y[16], Z[16], QV[16], KA[16], Kf[16];
+        mfma4(P, Am, zero, T1);
+        mfma4(P, G2, C2, T2);
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) PP[4 * r + c] = T2[4 * r + 2];
+        mfma4(Am, T1, CH, Q);
+        mfma4(G2, T1, zero, Y);
+        mfma4(G2, T2, CZ, Z);
+        mfma4(Am, PP, GQ, QV);
+        const double R00 = Z[0], R01 = Z[1], rt0 = Z[2], R11 = Z[5], rt1 = Z[6];
+        const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+        double Xa[16] = {0};
+        Xa[0] = -R11; Xa[1] = R01; Xa[4] = R01; Xa[5] = -R00;
+        mfma4(Xa, Y, zero, KA);
+        for (int q = 0; q < 16; ++q) Kf[q] = KA[q] * (q < 8 ? idet : 0.0);
+        for (int q = 0; q < 8; ++q) s->K[q] = Kf[q];
+        s->Rn[0] = (-R11) * idet;
+        s->Rn[1] = R01 * idet;
+        s->Rn[2] = (-R00) * idet;
+        s->kk[0] = qfma(s->Rn[1], rt1, s->Rn[0] * rt0);
+        s->kk[1] = qfma(s->Rn[2], rt1, s->Rn[1] * rt0);
+        if (k > 0) {
+            /* P = Q~ + S~'K keeps its upper triangle; the lower one is the same products transposed
+             * (K'S~ + Q~', with Q~' = T1'A + Hx: bit for bit the transposes), so P stays symmetric as the
+             * lane walk's */
+            double RT[16] = {0}, QT[16], PT[16];
+            for (int c = 0; c < 4; ++c) { RT[c] = rt0; RT[4 + c] = rt1; }
+            mfma4(T1, Am, CH, QT);
+            mfma4(Y, Kf, Q, P);
+            mfma4(Kf, Y, QT, PT);
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < r; ++c) P[4 * r + c] = PT[4 * r + c];
+            mfma4(Kf, RT, QV, pv);
+        }
+    }
+}
+
 static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], int factor)
 {
     const int N = p->N, S = p->S;
@@ -966,6 +1056,8 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
         delta_scan_s2(p, st, gx3, gu);
     } else if (S == 2 && factor && p->factor_scan) {
         factor_scan_s2(p, st, hx3, hu, gx3, gu);
+    } else if (S == 1 && factor && p->mfma_walk) {
+        factor_walk_mfma(p, st, hx3, hu, gx3, gu);
     } else {
         if (factor) {
             for (int i = 0; i < 10; ++i) P[i] = 0.0;

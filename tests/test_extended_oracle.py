@@ -44,10 +44,10 @@ def test_adjudicated_lanes_config2(orc):
     from oracle.oracle import Oracle, make_opts
     g = json.load(open(os.path.join(GOLDEN, "ext_adjudication_c2.json")))
     s = g["summary"]
-    # the scan: 560 of 5 904 lanes disagree by > 1e-6; in exact arithmetic (quad) the twin and the
-    # literal are right about equally often on them, and on the one lane stable under every probe
+    # the scan: 573 of 5 904 lanes disagree by > 1e-6; in exact arithmetic (quad) the twin and the
+    # literal are right about equally often on them (90 and 80), and on the one lane stable under every probe
     # in both implementations the extended-precision answer is the twin's (the GPU's)
-    assert s["disagreeing_lanes"] == 560 and s["lanes"] == 5904
+    assert s["disagreeing_lanes"] == 573 and s["lanes"] == 5904
     assert abs(s["all_disagreeing"]["twin"] - s["all_disagreeing"]["literal"]) <= 10
     assert s["disagreeing_stable_in_both"] == {"twin": 1, "literal": 0, "both": 0, "neither": 0}
     lanes = np.array([l["lane"] for l in g["lanes"]])

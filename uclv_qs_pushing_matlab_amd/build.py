@@ -20,8 +20,10 @@ ARCH = os.environ.get("QSP_OFFLOAD_ARCH", "gfx950")
 # run at 256 VGPRs + ~200 AGPRs): 16 fewer AGPR copies per factor-walk step, scratch 68 -> 0 B/lane,
 # 92.9k -> 94.5k solves/s, bit-identical (profiles/r04/ab_s2_regclass.txt); the S = 1 kernels'
 # code is unchanged.
+# -amdgpu-mfma-vgpr-form: the matrix-core factor walk's operands and results in VGPRs (the S = 1
+# kernels keep two waves per SIMD only without AGPRs).
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-         "-mllvm", "-greedy-regclass-priority-trumps-globalness"]
+         "-mllvm", "-greedy-regclass-priority-trumps-globalness", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def source_digest():

@@ -78,6 +78,8 @@ struct qsp_solver {
     int parts_req = 0;
     int fused_req = -1;            // QSP_FUSED_LOOP (-1: auto)
     bool nopack = false;           // QSP_PACKING=0: instances in lane order (developer A/B of the wave packing)
+    bool mfw = true;               // QSP_MFMA_WALK=0: the lane walk at 15 <= N <= 31 too (developer A/B; rounds
+                                   // differently, so the oracle twin does not follow it)
     int cus = 256;                 // compute units of the device (hipDeviceProp multiProcessorCount)
 };
 
@@ -132,6 +134,7 @@ static void fill_params(qsp_solver* s) {
     p.qp_tol_eq = s->o.qp_tol_eq;
     p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
     p.factor_scan = s->o.factor_scan ? 1 : 0;
+    p.mfma_walk = s->mfw ? 1 : 0;
     p.qp_stall_iters = s->o.qp_stall_iters;
     p.qp_stall_alpha = s->o.qp_stall_alpha;
     p.qp_mu_max = s->o.qp_mu_max;
@@ -440,6 +443,8 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     // never wrote shows up as NaN (tests/test_gpu_errors.py)
     if (const char* fl = std::getenv("QSP_FUSED_LOOP")) s->fused_req = (fl[0] == '1') ? 1 : (fl[0] == '0' ? 0 : -1);
     if (const char* pk = std::getenv("QSP_PACKING")) s->nopack = pk[0] == '0';
+    if (const char* mw = std::getenv("QSP_MFMA_WALK")) s->mfw = mw[0] != '0';
+    s->p.mfma_walk = s->mfw ? 1 : 0;
     const char* pz = std::getenv("QSP_DEBUG_POISON");
     s->poison = pz && pz[0] == '1';
     if (s->poison) {

@@ -157,15 +157,18 @@ enum LdsField : int {
     F_LM = 6,     // 6  multipliers
     F_V = 12,     // 3  bounded components of the SQP iterate (s_k, u_n, u_t)
     F_DU = 15,    // 2  damped QP control step
-    F_VA = 17,    // 3  affine-predictor bounded components (ds, dun, dut)
-    F_VN = 20,    // 3  corrector bounded components
-    F_DX = 17,    // 4  final QP state step (written after the IPM: aliases F_VA / F_VN)
-    F_HG = 23,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
-    F_RT = 29,    // 6  1 / slack, refreshed whenever the slacks change
+    F_RT = 17,    // 6  1 / slack, refreshed whenever the slacks change
+    F_VA = 23,    // 3  affine-predictor bounded components (ds, dun, dut)
+    F_VN = 26,    // 3  corrector bounded components
+    F_DX = 23,    // 4  final QP state step (written after the IPM: aliases F_VA / F_VN)
+    F_HG = 29,    // 6  barrier Hessian (0..2) / gradient (3..5) additions
     F_COUNT = 35
 };
+// S = 1: the matrix-core factor walk's stage records overlay F_VA .. F_HG (free while the predictor
+// factorises) and MFW_EXTRA more fields (factor_walk_mfma)
+constexpr int MFW_EXTRA = 2;
 template <int S>
-constexpr int lds_bytes() { return F_COUNT * S * BLOCK * 8; }
+constexpr int lds_bytes() { return (F_COUNT * S + (S == 1 ? MFW_EXTRA : 0)) * BLOCK * 8; }
 
 template <int S>
 struct Stage {
@@ -370,6 +373,170 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
     const double n2 = qfma(B[5], du[1], qfma(B[4], du[0], qfma(a[4], dx[3], bb[2] + dx[2])));
     const double n3 = qfma(B[7], du[1], qfma(B[6], du[0], qfma(a[5], dx[3], bb[3])));
     dx[0] = n0; dx[1] = n1; dx[2] = n2; dx[3] = n3;
+}
+
+// ------------------------------------- S = 1: the factorisation on the FP64 matrix cores
+// The factor walk's step is a handful of 4x4 products, which v_mfma_f64_4x4x4_4b_f64 computes for
+// four independent blocks of 16 lanes at once: lane l holds element (l >> 4, l & 3) of block
+// (l >> 2) & 3 of each operand, and the A operand is read transposed (mfma4(X, Y, C) = X'Y + C per
+// block; scripts/ubench/mfma_f64_probe.hip).  Block b walks instance min(b, G - 1) of the wave with
+// its value function held one element per lane, so a step costs eleven matrix-core products and
+// ~45 VALU instead of the lane walk's ~210 VALU on 1 of 21 lanes.
+// The stage data reaches the blocks through LDS: before the walk every stage lane writes a
+// 27-double record (MfwSlot) over the fields that are free while the predictor factorises (F_VA ..
+// F_HG and MFW_EXTRA more); the block lanes read their operand elements from it, one step ahead,
+// and write the stage's K and [R~ | r~] back over its first 16 slots, which the stage lane collects
+// after the walk (forming -R~^-1 and kk itself, in parallel).  The records of a wave's G instances do not fit at once: the walk runs in two
+// phases (stages H .. N-1 with the terminal record, then 0 .. H-1).
+enum MfwSlot : int { R_A = 0, R_B = 6, R_BB = 14, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
+enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 of Z = [R~ | r~ | .]
+static_assert((F_COUNT - F_VA + MFW_EXTRA) * BLOCK >= 33 * MFW_REC, "records of G (N/2 + 1) stages, 15 <= N <= 31");
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {   // a'b + c per 4x4 block
+    return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+template <int CTRL>
+__device__ __forceinline__ double quad_bcast(double v) {   // DPP quad_perm: one lane of each quad to all four
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Which horizons factorise on the matrix cores: one instance per 16-lane block (G <= 4: N >= 15) and
+// one stage per lane (N <= 31); the kernels take it as their ALT variant (mfw_use).
+__host__ __device__ __forceinline__ bool mfw_fits(int N) { return N >= 15 && N <= 31; }
+__host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p) { return p.mfma_walk != 0 && mfw_fits(p.N); }
+
+__device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams& p, Stage<1>& st, double hx3,
+                                                 const double hu[2], double gx3, const double gu[2]) {
+    const int N = c.N, G = 64 / c.L;
+    const int H = (N + 1) / 2, CM = N + 1 - H;   // phase split; records per instance and phase
+    double* const reg = st.lds - (threadIdx.x & 63) + F_VA * BLOCK;
+    // block-lane geometry and the record slot of each operand element (-1: structural constant)
+    // (an opaque lane id: derived from c.lane, the geometry would be hoisted out of the IPM loop and
+    // kept live through it)
+    int l = c.lane;
+    asm volatile("" : "+v"(l));
+    const int b = (l >> 2) & 3, r = l >> 4, cc = l & 3;
+    const int bg = b < G ? b : G - 1;
+    const bool wr = b < G;
+    int ao = -1;
+    if (cc >= 2 && r < 2) ao = R_A + 2 * r + (cc - 2);
+    else if (cc == 3 && r >= 2) ao = R_A + 2 + r;
+    const double aconst = r == cc ? 1.0 : 0.0;
+    const int go = cc < 2 ? R_B + 2 * r + cc : (cc == 2 ? R_BB + r : -1);
+    int xo = -1;   // the C operand of Q (Hx: only hx3 varies) and of Z (Hu, gu) share one read
+    if (r == 3 && cc == 3) xo = R_HX3;
+    else if (r < 2 && r == cc) xo = R_HU + r;
+    else if (r < 2 && cc == 2) xo = R_GU + r;
+    const double hxc = r == 0 ? p.tau * p.W[0] : (r == 1 ? p.tau * p.W[1] : p.tau * p.W[2]);
+    const int ao_ = ao < 0 ? 0 : ao, go_ = go < 0 ? 0 : go, xo_ = xo < 0 ? 0 : xo;
+    double P = 0.0, pv = 0.0;
+    for (int ph = 0; ph < 2; ++ph) {
+        const int kb = ph == 0 ? H : 0, ke = ph == 0 ? N : H - 1;   // records kb .. ke
+        // publish: stage lane (grp, k) writes its record
+        if (c.grp < G && c.lig >= kb && c.lig <= ke) {
+            double* rw = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+            if (c.lig < N) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[0][q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[0][q];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[0][q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[0][q];
+                rw[R_GX + 3] = gx3;
+                rw[R_HX3] = hx3;
+                rw[R_HU] = hu[0];
+                rw[R_HU + 1] = hu[1];
+                rw[R_GU] = gu[0];
+                rw[R_GU + 1] = gu[1];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[0][q];   // terminal: p_N = g_N
+            }
+        }
+        const double* rb = reg + bg * CM * MFW_REC;   // this block's records of the phase
+        if (ph == 0) {
+            P = r == cc ? (r == 0 ? p.We[0] : (r == 1 ? p.We[1] : (r == 2 ? p.We[2] : p.We[3]))) : 0.0;
+            pv = rb[(N - kb) * MFW_REC + R_GX + r];
+        }
+        const int kf = ph == 0 ? N - 1 : H - 1;
+        double va = rb[(kf - kb) * MFW_REC + ao_], vg = rb[(kf - kb) * MFW_REC + go_];
+        double vx = rb[(kf - kb) * MFW_REC + xo_], vq = rb[(kf - kb) * MFW_REC + R_GX + r];
+        for (int k = kf; k >= kb; --k) {
+            double* rk = reg + (bg * CM + (k - kb)) * MFW_REC;
+            const double Am = ao >= 0 ? va : aconst;
+            const double G2 = go >= 0 ? vg : 0.0;
+            const double CH = r == cc ? (r == 3 ? vx : hxc) : 0.0;
+            const double CZ = xo >= 0 && r < 2 ? vx : 0.0;
+            const double gq = vq;
+            if (k > kb) {   // the next step's operand elements
+                const double* rn = rk - MFW_REC;
+                va = rn[ao_]; vg = rn[go_]; vx = rn[xo_]; vq = rn[R_GX + r];
+            }
+            const double T1 = mfma4(P, Am, 0.0);                    // P'A
+            const double T2 = mfma4(P, G2, cc == 2 ? pv : 0.0);     // P'[B | b | 0] + [0 | 0 | p | 0]
+            const double pp = quad_bcast<0xAA>(T2);                 // (p + P'b)[r] across the row
+            const double Q = mfma4(Am, T1, CH);                     // Hx + A'P'A
+            const double Y = mfma4(G2, T1, 0.0);                    // rows 0, 1: S~ = B'P'A
+            const double Z = mfma4(G2, T2, CZ);                     // rows 0, 1: [R~ | r~]
+            const double qv = mfma4(Am, pp, gq);                    // q~ = gx + A'pp (across the row)
+            // R~ and r~ on the lanes of rows 0 and 1: v_permlane16_swap puts row 0 of Z into rows 0, 1
+            // of its first result and row 1 into rows 0, 1 of the second; quad broadcasts pick columns
+            const auto slo = __builtin_amdgcn_permlane16_swap(__double2loint(Z), __double2loint(Z), false, false);
+            const auto shi = __builtin_amdgcn_permlane16_swap(__double2hiint(Z), __double2hiint(Z), false, false);
+            const double w0 = __hiloint2double(shi[0], slo[0]), w1 = __hiloint2double(shi[1], slo[1]);
+            const double R00 = quad_bcast<0x00>(w0), R01 = quad_bcast<0x55>(w0), rt0 = quad_bcast<0xAA>(w0);
+            const double R11 = quad_bcast<0x55>(w1), rt1 = quad_bcast<0xAA>(w1);
+            // K = -R~^-1 S~ = (Xa'S~) / det with Xa = -adj R~: the product does not wait for the reciprocal
+            const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+            const double Xa = (r < 2 && cc < 2) ? (r != cc ? R01 : (r == 0 ? -R11 : -R00)) : 0.0;
+            const double Kf = mfma4(Xa, Y, 0.0) * (r < 2 ? idet : 0.0);   // rows 0, 1: K; rows 2, 3: 0
+            // (rows 2, 3 hold no R~: their idet is not finite, and Kf's zero rows enter P and p)
+            // stage k's K and [R~ | r~] over the record's first slots (its operands are already read)
+            if (wr && r < 2) {
+                rk[O_K + 4 * r + cc] = Kf;
+                rk[O_Z + 4 * r + cc] = Z;
+            }
+            if (k > 0) {   // P_k, p_k (nothing reads P_0, p_0)
+                // P keeps its upper triangle and takes the lower one from the transposed products
+                // (K'S~ + Q~', Q~' = T1'A + Hx: the same products in the same order, so bit for bit the
+                // transpose): a symmetric P as the lane walk's.  Left to drift apart, the two triangles
+                // cost the ill-conditioned QPs up to 1e3x the walk's error (tests/test_gpu_parity.py).
+                const double RT = r == 0 ? rt0 : (r == 1 ? rt1 : 0.0);
+                const double Qt = mfma4(T1, Am, CH);
+                const double Pu = mfma4(Y, Kf, Q);                  // Q~ + S~'K
+                const double Pl = mfma4(Kf, Y, Qt);                 // its transpose
+                P = r <= cc ? Pu : Pl;
+                pv = mfma4(Kf, RT, qv);                             // q~ + K'r~
+            }
+        }
+        // collect: stage lane (grp, k < N) takes its factors
+        if (c.grp < G && c.lig >= kb && c.lig <= ke && c.lig < N) {
+            const double* rr = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) st.K[0][q] = rr[O_K + q];
+            // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
+            const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
+            const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+            st.Rn[0][0] = (-R11) * idet;
+            st.Rn[0][1] = R01 * idet;
+            st.Rn[0][2] = (-R00) * idet;
+            st.kk[0][0] = qfma(st.Rn[0][1], rt1, st.Rn[0][0] * rt0);
+            st.kk[0][1] = qfma(st.Rn[0][2], rt1, st.Rn[0][1] * rt0);
+        }
+    }
+    // the overlaid fields read later: the terminal lanes' F_VA / F_VN slots stay zero (the forward
+    // passes write them on the stage lanes only; qp_ipm's start defines them)
+    if (c.lig >= N) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            st.f(F_VA, 0, q) = 0.0;
+            st.f(F_VN, 0, q) = 0.0;
+        }
+    }
 }
 
 // ------------------------------------------------ S = 2: the affine passes as scans
@@ -708,7 +875,7 @@ __device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const dou
 // Backward pass over the group (factorisation, or the corrector's difference recursion),
 // then forward pass writing the bounded components of the solution into LDS field `out`
 // (F_VA / F_VN).
-template <int S, bool FACTOR, bool SCAN = false>
+template <int S, bool FACTOR, bool ALT = false>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
                                               int out, double (&M)[S][16]) {
     double P[10], pv[4];
@@ -813,7 +980,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 st.kk[ls][1] += dkk[1];
             }
         }
-    } else if constexpr (S == 2 && FACTOR && SCAN) {
+    } else if constexpr (S == 2 && FACTOR && ALT) {
         // factorisation as a suffix scan of the lanes' value-function elements: lane j combines its
         // two stages' elements (slot 0's, then slot 1's; the terminal element where k = N, none past
         // it), Hillis-Steele levels give E_{2j:N}, the next lane's result E_{2j+2:N} gives slot 1's
@@ -865,6 +1032,8 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 ric_factor_step(st.a[0], st.B[0], st.bb[0], Hx, hu[0], gx, gu[0], Pn, pn, st.K[0], st.Rn[0], st.kk[0], false);
             }
         }
+    } else if constexpr (S == 1 && FACTOR && ALT) {
+        factor_walk_mfma(c, p, st, hx3[0], hu[0], gx3[0], gu[0]);
     } else
     for (int j = c.L - 1; j >= 0; --j) {
         // Lanes above j already hold their final factors and sit the step out (exec
@@ -1035,7 +1204,7 @@ enum QpExit : int { QP_EXIT_CONV = 0, QP_EXIT_CAP = 1, QP_EXIT_STALL = 2, QP_EXI
 // (1 - alpha), so each is its start value times prod(1 - alpha) (tracked, not recomputed:
 // r0 = bound residual of the floored slacks, rg0 = max|g + C' lam|, rb0 = max(|dx0|, |b|)); the
 // test r * prod < tol is applied as prod < min(tol / r) over the three.
-template <int S, bool SCAN = false>
+template <int S, bool ALT = false>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], int& exit,
                       bool skip = false) {
     const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
@@ -1113,7 +1282,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls);
         double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
-        riccati_solve<S, true, SCAN>(c, p, st, dx0, F_VA, M);
+        riccati_solve<S, true, ALT>(c, p, st, dx0, F_VA, M);
         // affine directions: computed once, kept in registers through the corrector
         double at[S][6], al[S][6];
         double num = 1.0, den = 1.0;
@@ -1130,7 +1299,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         // ---- corrector
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, p, st, ls, at[ls], al[ls], smu);
-        riccati_solve<S, false, SCAN>(c, p, st, dx0, F_VN, M);
+        riccati_solve<S, false, ALT>(c, p, st, dx0, F_VN, M);
         double dt[S][6], dl[S][6];
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
@@ -1479,7 +1648,7 @@ __device__ __forceinline__ bool qp_outcome(const SolveArgs& A, const Ctx& c, con
     return failed;
 }
 
-template <int S, bool MERIT = false, bool LIN = false, bool SCAN = false>
+template <int S, bool MERIT = false, bool LIN = false, bool ALT = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -1591,7 +1760,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
     }
     int exit;
-    const int nit = qp_ipm<S, SCAN>(c, p, st, dx0, exit, skip);
+    const int nit = qp_ipm<S, ALT>(c, p, st, dx0, exit, skip);
     qp_rollout<S>(c, st, dx0);
     const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
     if (A.wnit && c.real && c.lig == 0) {
@@ -1666,7 +1835,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
 // wave of the batch (no packing sort, no grid-wide boundary between SQP iterations).  The
 // per-iteration arithmetic is qp_step_kernel<S, false, true>'s (same helpers, same order), so
 // the results are bit-identical to the per-iteration launches (tests/test_gpu_fullsize.py).
-template <int S, bool SCAN = false>
+template <int S, bool ALT = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArgs A) {
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
@@ -1750,7 +1919,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
         for (int q = 0; q < 4; ++q) dx0[q] = A.wx0[(size_t)iv * 4 + q] - X[q];
         const bool skip = stopped || !c.real;
         int exit;
-        const int nit = qp_ipm<S, SCAN>(c, p, st, dx0, exit, skip);
+        const int nit = qp_ipm<S, ALT>(c, p, st, dx0, exit, skip);
         qp_rollout<S>(c, st, dx0);
         const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
         qp_adjoint_store<S>(c, p, st, A.PI_out + (size_t)iv * N * 4, c.real && !skip && !failed,
@@ -2311,30 +2480,31 @@ static hipError_t lds_attr_once(const void* kernel, int bytes, std::atomic<uint6
 
 // LIN: the SQP iteration's linearisation runs inside the QP kernel (nlp_mode 0); without
 // it the kernel reads the stage data the workspace holds (qsp_qp_solve).
-// SCAN (S = 2 only, SolveParams::factor_scan): the factorisation runs as an associative scan
-template <int S, bool LIN, bool SCAN = false>
+// ALT: the alternative factorisation of the stage count — S = 2: the associative scan
+// (SolveParams::factor_scan); S = 1: the walk on the matrix cores (mfw_use)
+template <int S, bool LIN, bool ALT = false>
 static hipError_t launch_qp_step(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN, SCAN>, lds_bytes<S>(), attr);
+    const hipError_t e = lds_attr_once((const void*)qp_step_kernel<S, false, LIN, ALT>, lds_bytes<S>(), attr);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((qp_step_kernel<S, false, LIN, SCAN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
+    hipLaunchKernelGGL((qp_step_kernel<S, false, LIN, ALT>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a, it);
     return hipGetLastError();
 }
 
-template <int S, bool SCAN = false>
+template <int S, bool ALT = false>
 static hipError_t launch_sqp_loop(const SolveArgs& a, hipStream_t stream) {
     const int L = (a.p.N + S) / S;
     const int G = 64 / L;
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0};
-    const hipError_t e = lds_attr_once((const void*)sqp_loop_kernel<S, SCAN>, lds_bytes<S>(), attr);
+    const hipError_t e = lds_attr_once((const void*)sqp_loop_kernel<S, ALT>, lds_bytes<S>(), attr);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((sqp_loop_kernel<S, SCAN>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a);
+    hipLaunchKernelGGL((sqp_loop_kernel<S, ALT>), dim3(blocks), dim3(BLOCK), lds_bytes<S>(), stream, a);
     return hipGetLastError();
 }
 
@@ -2351,7 +2521,10 @@ int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus) {
 
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
-        case 1: return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
+        case 1:
+            if (mfw_use(a.p))
+                return lin ? launch_qp_step<1, true, true>(a, it, stream) : launch_qp_step<1, false, true>(a, it, stream);
+            return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
         case 2:
             if (a.p.factor_scan)
                 return lin ? launch_qp_step<2, true, true>(a, it, stream) : launch_qp_step<2, false, true>(a, it, stream);
@@ -2367,10 +2540,16 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     const int G = 64 / L;
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
-    static std::atomic<uint64_t> attr{0};
-    const hipError_t ea =lds_attr_once((const void*)qp_step_kernel<1, true, true>, lds_bytes<1>(), attr);
-    if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    static std::atomic<uint64_t> attr{0}, attr_alt{0};
+    if (mfw_use(a.p)) {
+        const hipError_t ea = lds_attr_once((const void*)qp_step_kernel<1, true, true, true>, lds_bytes<1>(), attr_alt);
+        if (ea != hipSuccess) return ea;
+        hipLaunchKernelGGL((qp_step_kernel<1, true, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    } else {
+        const hipError_t ea = lds_attr_once((const void*)qp_step_kernel<1, true, true>, lds_bytes<1>(), attr);
+        if (ea != hipSuccess) return ea;
+        hipLaunchKernelGGL((qp_step_kernel<1, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(merit_ls_kernel, dim3(waves), dim3(64), 0, stream, a);   // one wave per workgroup
@@ -2444,7 +2623,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e == hipSuccess) e = mark();
     if (fused) {
         if (e == hipSuccess)
-            e = S == 1 ? launch_sqp_loop<1>(as, stream)
+            e = S == 1 ? (mfw_use(as.p) ? launch_sqp_loop<1, true>(as, stream) : launch_sqp_loop<1>(as, stream))
                        : (as.p.factor_scan ? launch_sqp_loop<2, true>(as, stream) : launch_sqp_loop<2>(as, stream));
         ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
