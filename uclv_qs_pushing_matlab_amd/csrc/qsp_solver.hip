@@ -478,10 +478,11 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             }
             const double T1 = mfma4(P, Am, 0.0);                    // P'A
             const double T2 = mfma4(P, G2, cc == 2 ? pv : 0.0);     // P'[B | b | 0] + [0 | 0 | p | 0]
-            const double pp = quad_bcast<0xAA>(T2);                 // (p + P'b)[r] across the row
-            const double Q = mfma4(Am, T1, CH);                     // Hx + A'P'A
             const double Y = mfma4(G2, T1, 0.0);                    // rows 0, 1: S~ = B'P'A
             const double Z = mfma4(G2, T2, CZ);                     // rows 0, 1: [R~ | r~]
+            const double Q = mfma4(Am, T1, CH);                     // Hx + A'P'A
+            const double Qt = mfma4(T1, Am, CH);                    // its transpose (below)
+            const double pp = quad_bcast<0xAA>(T2);                 // (p + P'b)[r] across the row
             const double qv = mfma4(Am, pp, gq);                    // q~ = gx + A'pp (across the row)
             // R~ and r~ on the lanes of rows 0 and 1: v_permlane16_swap puts row 0 of Z into rows 0, 1
             // of its first result and row 1 into rows 0, 1 of the second; quad broadcasts pick columns
@@ -491,9 +492,11 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             const double R00 = quad_bcast<0x00>(w0), R01 = quad_bcast<0x55>(w0), rt0 = quad_bcast<0xAA>(w0);
             const double R11 = quad_bcast<0x55>(w1), rt1 = quad_bcast<0xAA>(w1);
             // K = -R~^-1 S~ = (Xa'S~) / det with Xa = -adj R~: the product does not wait for the reciprocal
-            const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+            const double det = qfma(R00, R11, -(R01 * R01));
             const double Xa = (r < 2 && cc < 2) ? (r != cc ? R01 : (r == 0 ? -R11 : -R00)) : 0.0;
-            const double Kf = mfma4(Xa, Y, 0.0) * (r < 2 ? idet : 0.0);   // rows 0, 1: K; rows 2, 3: 0
+            const double Ka = mfma4(Xa, Y, 0.0);
+            const double idet = rcp(det);
+            const double Kf = Ka * (r < 2 ? idet : 0.0);            // rows 0, 1: K; rows 2, 3: 0
             // (rows 2, 3 hold no R~: their idet is not finite, and Kf's zero rows enter P and p)
             // stage k's K and [R~ | r~] over the record's first slots (its operands are already read)
             if (wr && r < 2) {
@@ -506,7 +509,6 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                 // transpose): a symmetric P as the lane walk's.  Left to drift apart, the two triangles
                 // cost the ill-conditioned QPs up to 1e3x the walk's error (tests/test_gpu_parity.py).
                 const double RT = r == 0 ? rt0 : (r == 1 ? rt1 : 0.0);
-                const double Qt = mfma4(T1, Am, CH);
                 const double Pu = mfma4(Y, Kf, Q);                  // Q~ + S~'K
                 const double Pl = mfma4(Kf, Y, Qt);                 // its transpose
                 P = r <= cc ? Pu : Pl;
