@@ -722,7 +722,12 @@ def main():
                    "global_batch": total, "N": N, "sqp_iters": K, "qp_iters_max": args.qp_iters,
                    "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
-                              "stream_parts": parts, "factor_scan": bool(args.factor_scan and S_layout == 2)},
+                              "stream_parts": parts, "factor_scan": bool(args.factor_scan and S_layout == 2),
+                              # the library's choice (qsp_solver.hip mfw_use): one stage per lane at
+                              # 15 <= N <= 31 factorises on the FP64 matrix cores
+                              "factor_walk": ("matrix cores (v_mfma_f64_4x4x4_4b_f64)"
+                                              if S_layout == 1 and 15 <= N <= 31 and os.environ.get("QSP_MFMA_WALK", "1") != "0"
+                                              else ("associative scan" if args.factor_scan and S_layout == 2 else "lane walk"))},
                    "parallelism": f"dp{world} (contiguous lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),

@@ -10,7 +10,10 @@ records both margins (or_set_kkt_diag, oracle/qsp_oracle.c): kkt[18] = min over 
 dphi| / |phi0|.  Measured on the twin (= the device bit for bit) over 4 096 lanes x 2 steps, every
 status or sqp_iter difference on a probe-stable lane had an Armijo margin below 3e-15 (most 0: a step
 whose merit change is below rounding) or a KKT residual within a factor 10 of tol; none remained in
-the far stratum below."""
+the far stratum below.  The margins are the literal's: a lane whose device-side
+decision sits at its own edge shows as a device answer that moves under the probes, which the GPU
+test also excludes (one lane of the 4 096 x 2 with the matrix-core factor walk: block 3, lane 452,
+step 2, sqp_iter 29 or 30 by the probe's sign on the twin, with either factor walk)."""
 import numpy as np
 
 KKT_DIAG = 22          # doubles per lane of or_set_kkt_diag
