@@ -173,6 +173,32 @@ def test_layouts_differ_by_rounding_only(twin):
     np.testing.assert_allclose(u[0], u[1], rtol=0, atol=1e-12)
 
 
+def test_mfma_walk_matches_lane_walk(twin, monkeypatch):
+    """The matrix-core factorisation (the default at one stage per lane, 15 <= N <= 31) against the lane
+    walk (QSP_MFMA_WALK=0), both measured against the literal formulas in __float128: three SQP-RTI
+    iterations of 64 lanes, mixed shapes, at the range's lower edge and the bench horizon.  The two walks
+    associate every product differently (their answers part after the first iteration) and are equally
+    accurate: the same lanes sit beyond 1e-9 of exact arithmetic (the ill-conditioned ones, also for the
+    literal restatement), and the median error is the same.  Measured: 4 and 3 such lanes, medians
+    3.1e-13 / 3.8e-13 for the matrix cores, 3.1e-13 / 5.5e-13 for the lane walk."""
+    nb = 64
+    x0 = config2_x0(nb, 13)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    lit = Oracle(NAMES)
+    for N in (15, 20):
+        op = make_opts(N=N, sqp_iters=3)
+        q = lit.controller_solve_ext(op, x0, traj, 1, lit.new_warm(nb, N), shape_id=sid, precision="quad")["u0"]
+        err = {}
+        for mw in ("1", "0"):
+            monkeypatch.setenv("QSP_MFMA_WALK", mw)
+            u = twin.controller_solve(op, x0, traj, 1, twin.new_warm(nb, N), shape_id=sid)["u0"]
+            err[mw] = np.abs(u - q).max(1)
+        assert not np.array_equal(err["1"], err["0"]), f"N={N}: the two walks should round differently"
+        assert np.array_equal(err["1"] > 1e-9, err["0"] > 1e-9), f"N={N}"
+        assert np.median(err["1"]) < 2 * np.median(err["0"]) + 1e-15, (N, np.median(err["1"]), np.median(err["0"]))
+
+
 def test_s2_scans_across_horizons(twin):
     """The S = 2 layout's scans (forward and corrector-difference passes as Hillis-Steele scans over
     the group's lanes, at any lane count L = ceil((N+1)/2), powers of two or not) against the S = 1
