@@ -382,10 +382,17 @@ static void make_par(tw_par *p, const or_opts *o)
     p->qp_stall_iters = o->qp_stall_iters;
     p->s0_bound = o->stage0_s_bound ? 1 : 0;
     p->factor_scan = o->factor_scan ? 1 : 0;
-    /* the kernels factorise on the matrix cores at one stage per lane and 15 <= N <= 31 (mfw_use),
-     * unless the library's developer switch QSP_MFMA_WALK=0 selects the lane walk there too */
+    /* the kernels factorise on the matrix cores where one instance per 16-lane block and a phase's
+     * stage records fit (mfw_fits: one stage per lane at 15 <= N <= 31, two stages per lane from four
+     * instances per wave down), unless the library's developer switch QSP_MFMA_WALK=0 selects the lane
+     * walk there too */
     const char *mw = getenv("QSP_MFMA_WALK");
-    p->mfma_walk = p->S == 1 && p->N >= 15 && p->N <= 31 && !(mw && mw[0] == '0');
+    {
+        const int G = 64 / p->L, H = (p->N + 1) / 2, CM = p->N + 1 - H;
+        const int cap = (p->S == 1 ? 12 + 3 : 24 + 3) * 64;   /* F_VA .. F_HG per slot + MFW_EXTRA, x 64 lanes */
+        const int fits = G <= 4 && G * CM * 27 <= cap && (p->S == 2 || (p->N >= 15 && p->N <= 31));
+        p->mfma_walk = fits && !(mw && mw[0] == '0');
+    }
     p->Ts = o->Ts;
     p->tau = o->tau;
     memcpy(p->W, o->W, sizeof p->W);
@@ -1056,7 +1063,7 @@ static void riccati_solve(const tw_par *p, tw_stage *st, const double dx0[4], in
         delta_scan_s2(p, st, gx3, gu);
     } else if (S == 2 && factor && p->factor_scan) {
         factor_scan_s2(p, st, hx3, hu, gx3, gu);
-    } else if (S == 1 && factor && p->mfma_walk) {
+    } else if (factor && p->mfma_walk) {
         factor_walk_mfma(p, st, hx3, hu, gx3, gu);
     } else {
         if (factor) {

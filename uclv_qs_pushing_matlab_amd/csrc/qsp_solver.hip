@@ -166,9 +166,9 @@ enum LdsField : int {
 };
 // S = 1: the matrix-core factor walk's stage records overlay F_VA .. F_HG (free while the predictor
 // factorises) and MFW_EXTRA more fields (factor_walk_mfma)
-constexpr int MFW_EXTRA = 2;
+constexpr int MFW_EXTRA = 3;
 template <int S>
-constexpr int lds_bytes() { return (F_COUNT * S + (S == 1 ? MFW_EXTRA : 0)) * BLOCK * 8; }
+constexpr int lds_bytes() { return (F_COUNT * S + MFW_EXTRA) * BLOCK * 8; }
 
 template <int S>
 struct Stage {
@@ -390,7 +390,8 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 // phases (stages H .. N-1 with the terminal record, then 0 .. H-1).
 enum MfwSlot : int { R_A = 0, R_B = 6, R_BB = 14, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
 enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 of Z = [R~ | r~ | .]
-static_assert((F_COUNT - F_VA + MFW_EXTRA) * BLOCK >= 33 * MFW_REC, "records of G (N/2 + 1) stages, 15 <= N <= 31");
+static_assert((F_COUNT - F_VA + MFW_EXTRA) * BLOCK >= 33 * MFW_REC, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
+static_assert(((F_COUNT - F_VA) * 2 + MFW_EXTRA) * BLOCK >= 64 * MFW_REC, "S = 2: records of G (N/2 + 1) stages, N <= 127");
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {   // a'b + c per 4x4 block
     return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -402,16 +403,28 @@ __device__ __forceinline__ double quad_bcast(double v) {   // DPP quad_perm: one
     return __hiloint2double(hi, lo);
 }
 
-// Which horizons factorise on the matrix cores: one instance per 16-lane block (G <= 4: N >= 15) and
-// one stage per lane (N <= 31); the kernels take it as their ALT variant (mfw_use).
-__host__ __device__ __forceinline__ bool mfw_fits(int N) { return N >= 15 && N <= 31; }
-__host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p) { return p.mfma_walk != 0 && mfw_fits(p.N); }
+// LDS doubles the stage records may occupy: F_VA .. F_HG of every slot plus the extra fields.
+template <int S>
+constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + MFW_EXTRA) * BLOCK; }
+// Which horizons factorise on the matrix cores: one instance per 16-lane block (G <= 4: at one
+// stage per lane N >= 15, at two always), the records of a phase in the region.  One stage per lane
+// takes the walk as its ALT kernel variant; two stages per lane by a uniform switch, since
+// ALT is the factorisation scan there.
+__host__ __device__ __forceinline__ bool mfw_fits(int N, int S) {
+    const int L = (N + S) / S, G = 64 / L, H = (N + 1) / 2, CM = N + 1 - H;
+    const int cap = S == 1 ? mfw_region<1>() : mfw_region<2>();
+    return G <= 4 && G * CM * MFW_REC <= cap && (S == 2 || (N >= 15 && N <= 31));
+}
+__host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p, int S) {
+    return p.mfma_walk != 0 && mfw_fits(p.N, S);
+}
 
-__device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams& p, Stage<1>& st, double hx3,
-                                                 const double hu[2], double gx3, const double gu[2]) {
+template <int S>
+__device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams& p, Stage<S>& st, const double (&hx3)[S],
+                                                 const double (&hu)[S][2], const double (&gx3)[S], const double (&gu)[S][2]) {
     const int N = c.N, G = 64 / c.L;
     const int H = (N + 1) / 2, CM = N + 1 - H;   // phase split; records per instance and phase
-    double* const reg = st.lds - (threadIdx.x & 63) + F_VA * BLOCK;
+    double* const reg = st.lds - (threadIdx.x & 63) + F_VA * S * BLOCK;
     // block-lane geometry and the record slot of each operand element (-1: structural constant)
     // (an opaque lane id: derived from c.lane, the geometry would be hoisted out of the IPM loop and
     // kept live through it)
@@ -434,27 +447,31 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     double P = 0.0, pv = 0.0;
     for (int ph = 0; ph < 2; ++ph) {
         const int kb = ph == 0 ? H : 0, ke = ph == 0 ? N : H - 1;   // records kb .. ke
-        // publish: stage lane (grp, k) writes its record
-        if (c.grp < G && c.lig >= kb && c.lig <= ke) {
-            double* rw = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
-            if (c.lig < N) {
+        // publish: the stage lanes write the records of their slots' stages
 #pragma unroll
-                for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[0][q];
+        for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
+            if (c.grp < G && k >= kb && k <= ke) {
+                double* rw = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+                if (k < N) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[0][q];
+                    for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[ls][q];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[0][q];
+                    for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[ls][q];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[0][q];
-                rw[R_GX + 3] = gx3;
-                rw[R_HX3] = hx3;
-                rw[R_HU] = hu[0];
-                rw[R_HU + 1] = hu[1];
-                rw[R_GU] = gu[0];
-                rw[R_GU + 1] = gu[1];
-            } else {
+                    for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[ls][q];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[0][q];   // terminal: p_N = g_N
+                    for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[ls][q];
+                    rw[R_GX + 3] = gx3[ls];
+                    rw[R_HX3] = hx3[ls];
+                    rw[R_HU] = hu[ls][0];
+                    rw[R_HU + 1] = hu[ls][1];
+                    rw[R_GU] = gu[ls][0];
+                    rw[R_GU + 1] = gu[ls][1];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[ls][q];   // terminal: p_N = g_N
+                }
             }
         }
         const double* rb = reg + bg * CM * MFW_REC;   // this block's records of the phase
@@ -515,28 +532,47 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                 pv = mfma4(Kf, RT, qv);                             // q~ + K'r~
             }
         }
-        // collect: stage lane (grp, k < N) takes its factors
-        if (c.grp < G && c.lig >= kb && c.lig <= ke && c.lig < N) {
-            const double* rr = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+        // collect: the stage lanes take their slots' factors (stages k < N)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) st.K[0][q] = rr[O_K + q];
-            // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
-            const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
-            const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
-            st.Rn[0][0] = (-R11) * idet;
-            st.Rn[0][1] = R01 * idet;
-            st.Rn[0][2] = (-R00) * idet;
-            st.kk[0][0] = qfma(st.Rn[0][1], rt1, st.Rn[0][0] * rt0);
-            st.kk[0][1] = qfma(st.Rn[0][2], rt1, st.Rn[0][1] * rt0);
+        for (int ls = 0; ls < S; ++ls) {
+            const int k = kof<S>(c, ls);
+            if (c.grp < G && k >= kb && k <= ke && k < N) {
+                const double* rr = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) st.K[ls][q] = rr[O_K + q];
+                // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
+                const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
+                const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+                st.Rn[ls][0] = (-R11) * idet;
+                st.Rn[ls][1] = R01 * idet;
+                st.Rn[ls][2] = (-R00) * idet;
+                st.kk[ls][0] = qfma(st.Rn[ls][1], rt1, st.Rn[ls][0] * rt0);
+                st.kk[ls][1] = qfma(st.Rn[ls][2], rt1, st.Rn[ls][1] * rt0);
+            }
         }
     }
-    // the overlaid fields read later: the terminal lanes' F_VA / F_VN slots stay zero (the forward
-    // passes write them on the stage lanes only; qp_ipm's start defines them)
-    if (c.lig >= N) {
+    // the overlaid fields read later: the terminal and padding slots' F_VA / F_VN stay zero (the
+    // forward passes write them on the stages k < N only; qp_ipm's start defines them)
+    // (one stage per lane: written as the lane test, which keeps the kernel at 247 registers; the
+    // unrolled slot loop, the same test, costs it the second wave per SIMD)
+    if constexpr (S == 1) {
+        if (c.lig >= N) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            st.f(F_VA, 0, q) = 0.0;
-            st.f(F_VN, 0, q) = 0.0;
+            for (int q = 0; q < 3; ++q) {
+                st.f(F_VA, 0, q) = 0.0;
+                st.f(F_VN, 0, q) = 0.0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int ls = 0; ls < S; ++ls) {
+            if (kof<S>(c, ls) >= N) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    st.f(F_VA, ls, q) = 0.0;
+                    st.f(F_VN, ls, q) = 0.0;
+                }
+            }
         }
     }
 }
@@ -1035,8 +1071,16 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             }
         }
     } else if constexpr (S == 1 && FACTOR && ALT) {
-        factor_walk_mfma(c, p, st, hx3[0], hu[0], gx3[0], gu[0]);
-    } else
+        factor_walk_mfma<1>(c, p, st, hx3, hu, gx3, gu);
+    } else {
+    bool walked = false;
+    if constexpr (S == 2 && FACTOR) {
+        if (mfw_use(p, 2)) {   // uniform (two stages per lane: ALT is the factorisation scan)
+            factor_walk_mfma<2>(c, p, st, hx3, hu, gx3, gu);
+            walked = true;
+        }
+    }
+    if (!walked)
     for (int j = c.L - 1; j >= 0; --j) {
         // Lanes above j already hold their final factors and sit the step out (exec
         // mask); lanes below j compute a throw-away step that their own turn overwrites.
@@ -1078,6 +1122,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
                 for (int i = 0; i < 4; ++i) pv[i] = wave_from_next(pv[i], pvc[i]);
             }
         }
+    }
     }
     if constexpr (S == 1) {
         // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
@@ -2524,7 +2569,7 @@ int sqp_fused_auto(int B, int N, int S, int nlp_mode, int cus) {
 static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t stream, bool lin) {
     switch (S) {
         case 1:
-            if (mfw_use(a.p))
+            if (mfw_use(a.p, 1))
                 return lin ? launch_qp_step<1, true, true>(a, it, stream) : launch_qp_step<1, false, true>(a, it, stream);
             return lin ? launch_qp_step<1, true>(a, it, stream) : launch_qp_step<1, false>(a, it, stream);
         case 2:
@@ -2543,7 +2588,7 @@ static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t strea
     const int waves = (a.nI + G - 1) / G;
     const int blocks = (waves * 64 + BLOCK - 1) / BLOCK;
     static std::atomic<uint64_t> attr{0}, attr_alt{0};
-    if (mfw_use(a.p)) {
+    if (mfw_use(a.p, 1)) {
         const hipError_t ea = lds_attr_once((const void*)qp_step_kernel<1, true, true, true>, lds_bytes<1>(), attr_alt);
         if (ea != hipSuccess) return ea;
         hipLaunchKernelGGL((qp_step_kernel<1, true, true, true>), dim3(blocks), dim3(BLOCK), lds_bytes<1>(), stream, a, it);
@@ -2625,7 +2670,7 @@ hipError_t launch_sqp(const SolveArgs& a, int S, hipStream_t stream, hipEvent_t*
     if (e == hipSuccess) e = mark();
     if (fused) {
         if (e == hipSuccess)
-            e = S == 1 ? (mfw_use(as.p) ? launch_sqp_loop<1, true>(as, stream) : launch_sqp_loop<1>(as, stream))
+            e = S == 1 ? (mfw_use(as.p, 1) ? launch_sqp_loop<1, true>(as, stream) : launch_sqp_loop<1>(as, stream))
                        : (as.p.factor_scan ? launch_sqp_loop<2, true>(as, stream) : launch_sqp_loop<2>(as, stream));
         ne = 2 * K + 1;
         if (e == hipSuccess) e = mark();
