@@ -389,7 +389,7 @@ static void make_par(tw_par *p, const or_opts *o)
     const char *mw = getenv("QSP_MFMA_WALK");
     {
         const int G = 64 / p->L, H = (p->N + 1) / 2, CM = p->N + 1 - H;
-        const int cap = (p->S == 1 ? 12 + 3 : 24 + 3) * 64;   /* F_VA .. F_HG per slot + MFW_EXTRA, x 64 lanes */
+        const int cap = (p->S == 1 ? 12 + 2 : 24 + 3) * 64;   /* F_VA .. F_HG per slot + mfw_extra, x 64 lanes */
         const int fits = G <= 4 && G * CM * 27 <= cap && (p->S == 2 || (p->N >= 15 && p->N <= 31));
         p->mfma_walk = fits && !(mw && mw[0] == '0');
     }

@@ -165,10 +165,13 @@ enum LdsField : int {
     F_COUNT = 35
 };
 // S = 1: the matrix-core factor walk's stage records overlay F_VA .. F_HG (free while the predictor
-// factorises) and MFW_EXTRA more fields (factor_walk_mfma)
-constexpr int MFW_EXTRA = 3;
+// factorises) and mfw_extra<S>() more fields (factor_walk_mfma)
+// (S = 1: two, so eight one-wave workgroups and a packing-sort workgroup still share a CU's LDS; S = 2:
+// three, every horizon up to N = 127)
 template <int S>
-constexpr int lds_bytes() { return (F_COUNT * S + MFW_EXTRA) * BLOCK * 8; }
+constexpr int mfw_extra() { return S == 1 ? 2 : 3; }
+template <int S>
+constexpr int lds_bytes() { return (F_COUNT * S + mfw_extra<S>()) * BLOCK * 8; }
 
 template <int S>
 struct Stage {
@@ -384,14 +387,14 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 // ~45 VALU instead of the lane walk's ~210 VALU on 1 of 21 lanes.
 // The stage data reaches the blocks through LDS: before the walk every stage lane writes a
 // 27-double record (MfwSlot) over the fields that are free while the predictor factorises (F_VA ..
-// F_HG and MFW_EXTRA more); the block lanes read their operand elements from it, one step ahead,
+// F_HG and mfw_extra<S>() more); the block lanes read their operand elements from it, one step ahead,
 // and write the stage's K and [R~ | r~] back over its first 16 slots, which the stage lane collects
 // after the walk (forming -R~^-1 and kk itself, in parallel).  The records of a wave's G instances do not fit at once: the walk runs in two
 // phases (stages H .. N-1 with the terminal record, then 0 .. H-1).
 enum MfwSlot : int { R_A = 0, R_B = 6, R_BB = 14, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
 enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 of Z = [R~ | r~ | .]
-static_assert((F_COUNT - F_VA + MFW_EXTRA) * BLOCK >= 33 * MFW_REC, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
-static_assert(((F_COUNT - F_VA) * 2 + MFW_EXTRA) * BLOCK >= 64 * MFW_REC, "S = 2: records of G (N/2 + 1) stages, N <= 127");
+static_assert((F_COUNT - F_VA + mfw_extra<1>()) * BLOCK >= 33 * MFW_REC, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
+static_assert(((F_COUNT - F_VA) * 2 + mfw_extra<2>()) * BLOCK >= 64 * MFW_REC, "S = 2: records of G (N/2 + 1) stages, N <= 127");
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {   // a'b + c per 4x4 block
     return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -405,7 +408,7 @@ __device__ __forceinline__ double quad_bcast(double v) {   // DPP quad_perm: one
 
 // LDS doubles the stage records may occupy: F_VA .. F_HG of every slot plus the extra fields.
 template <int S>
-constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + MFW_EXTRA) * BLOCK; }
+constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + mfw_extra<S>()) * BLOCK; }
 // Which horizons factorise on the matrix cores: one instance per 16-lane block (G <= 4: at one
 // stage per lane N >= 15, at two always), the records of a phase in the region.  One stage per lane
 // takes the walk as its ALT kernel variant; two stages per lane by a uniform switch, since
