@@ -450,30 +450,56 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     double P = 0.0, pv = 0.0;
     for (int ph = 0; ph < 2; ++ph) {
         const int kb = ph == 0 ? H : 0, ke = ph == 0 ? N : H - 1;   // records kb .. ke
-        // publish: the stage lanes write the records of their slots' stages
+        // publish: the stage lanes write the records of their slots' stages (one stage per lane written
+        // as the lane test: the slot loop, the same test, costs the S = 1 kernel 2 % in issue order)
+        if constexpr (S == 1) {
+            if (c.grp < G && c.lig >= kb && c.lig <= ke) {
+                double* rw = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+                if (c.lig < N) {
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            const int k = kof<S>(c, ls);
-            if (c.grp < G && k >= kb && k <= ke) {
-                double* rw = reg + (c.grp * CM + (k - kb)) * MFW_REC;
-                if (k < N) {
+                    for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[0][q];
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[ls][q];
+                    for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[0][q];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[ls][q];
+                    for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[0][q];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[ls][q];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[ls][q];
-                    rw[R_GX + 3] = gx3[ls];
-                    rw[R_HX3] = hx3[ls];
-                    rw[R_HU] = hu[ls][0];
-                    rw[R_HU + 1] = hu[ls][1];
-                    rw[R_GU] = gu[ls][0];
-                    rw[R_GU + 1] = gu[ls][1];
+                    for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[0][q];
+                    rw[R_GX + 3] = gx3[0];
+                    rw[R_HX3] = hx3[0];
+                    rw[R_HU] = hu[0][0];
+                    rw[R_HU + 1] = hu[0][1];
+                    rw[R_GU] = gu[0][0];
+                    rw[R_GU + 1] = gu[0][1];
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[ls][q];   // terminal: p_N = g_N
+                    for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[0][q];   // terminal: p_N = g_N
+                }
+            }
+        } else {
+    #pragma unroll
+            for (int ls = 0; ls < S; ++ls) {
+                const int k = kof<S>(c, ls);
+                if (c.grp < G && k >= kb && k <= ke) {
+                    double* rw = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+                    if (k < N) {
+    #pragma unroll
+                        for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[ls][q];
+    #pragma unroll
+                        for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[ls][q];
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[ls][q];
+    #pragma unroll
+                        for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[ls][q];
+                        rw[R_GX + 3] = gx3[ls];
+                        rw[R_HX3] = hx3[ls];
+                        rw[R_HU] = hu[ls][0];
+                        rw[R_HU + 1] = hu[ls][1];
+                        rw[R_GU] = gu[ls][0];
+                        rw[R_GU + 1] = gu[ls][1];
+                    } else {
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q) rw[R_GX + q] = st.g[ls][q];   // terminal: p_N = g_N
+                    }
                 }
             }
         }
@@ -536,21 +562,37 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             }
         }
         // collect: the stage lanes take their slots' factors (stages k < N)
+        if constexpr (S == 1) {
+            if (c.grp < G && c.lig >= kb && c.lig <= ke && c.lig < N) {
+                const double* rr = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
 #pragma unroll
-        for (int ls = 0; ls < S; ++ls) {
-            const int k = kof<S>(c, ls);
-            if (c.grp < G && k >= kb && k <= ke && k < N) {
-                const double* rr = reg + (c.grp * CM + (k - kb)) * MFW_REC;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) st.K[ls][q] = rr[O_K + q];
+                for (int q = 0; q < 8; ++q) st.K[0][q] = rr[O_K + q];
                 // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
                 const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
                 const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
-                st.Rn[ls][0] = (-R11) * idet;
-                st.Rn[ls][1] = R01 * idet;
-                st.Rn[ls][2] = (-R00) * idet;
-                st.kk[ls][0] = qfma(st.Rn[ls][1], rt1, st.Rn[ls][0] * rt0);
-                st.kk[ls][1] = qfma(st.Rn[ls][2], rt1, st.Rn[ls][1] * rt0);
+                st.Rn[0][0] = (-R11) * idet;
+                st.Rn[0][1] = R01 * idet;
+                st.Rn[0][2] = (-R00) * idet;
+                st.kk[0][0] = qfma(st.Rn[0][1], rt1, st.Rn[0][0] * rt0);
+                st.kk[0][1] = qfma(st.Rn[0][2], rt1, st.Rn[0][1] * rt0);
+            }
+        } else {
+    #pragma unroll
+            for (int ls = 0; ls < S; ++ls) {
+                const int k = kof<S>(c, ls);
+                if (c.grp < G && k >= kb && k <= ke && k < N) {
+                    const double* rr = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+    #pragma unroll
+                    for (int q = 0; q < 8; ++q) st.K[ls][q] = rr[O_K + q];
+                    // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
+                    const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
+                    const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
+                    st.Rn[ls][0] = (-R11) * idet;
+                    st.Rn[ls][1] = R01 * idet;
+                    st.Rn[ls][2] = (-R00) * idet;
+                    st.kk[ls][0] = qfma(st.Rn[ls][1], rt1, st.Rn[ls][0] * rt0);
+                    st.kk[ls][1] = qfma(st.Rn[ls][2], rt1, st.Rn[ls][1] * rt0);
+                }
             }
         }
     }
