@@ -167,21 +167,23 @@ def flops_per_solve(N, K, qp_iter_total):
 
 
 def cpu_baseline(x0, traj, shape_id, N, K, target_s, threads, nlp_mode=0, twin=True, qp_iters=20, idx=1,
-                 sample=None):
+                 sample=None, lane_walk=0):
     """The CPU restatement (port) timed on a bounded sample of the same workload (cold-start
     controller solves): the kernel-order twin (twin=True: the library's formulation on the CPU,
     OpenMP over lanes) or the literal oracle.  idx: index_time (scalar, or per lane).  sample: a
-    fixed lane count instead of the target_s time budget (no probe run)."""
+    fixed lane count instead of the target_s time budget (no probe run).  lane_walk=1: the twin
+    factorises in the lane walk's order (the fastest CPU formulation of the algorithm) instead of
+    emulating the matrix cores' (the bit-exact checker's order)."""
     from oracle.oracle import Oracle, make_opts
     orc = Oracle(SHAPES, twin=twin)
-    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=qp_iters)
+    op = make_opts(N=N, sqp_iters=K, nlp_mode=nlp_mode, qp_iters=qp_iters, lane_walk=lane_walk)
     idx_all = np.broadcast_to(np.asarray(idx, np.int32), (len(x0),))
 
     def run(sl, xx=None, K_run=K, nthreads=None, precision=None, **kw):
         xx = x0[sl] if xx is None else xx
         warm = orc.new_warm(len(xx), N)
         o = op if (K_run == K and not kw) else make_opts(N=N, sqp_iters=K_run, nlp_mode=nlp_mode,
-                                                         **dict(dict(qp_iters=qp_iters), **kw))
+                                                         **dict(dict(qp_iters=qp_iters, lane_walk=lane_walk), **kw))
         nt = threads if nthreads is None else nthreads
         if precision is not None:   # the literal restatement in long double / __float128 (oracle OR_EXT)
             return orc.controller_solve_ext(o, xx, traj, idx_all[sl], warm, shape_id=shape_id[sl], nthreads=nt,
@@ -545,6 +547,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] (B = 4 096) side measurement")
     ap.add_argument("--no-configs4", action="store_true", help="skip the configs[4] (N = 50, B = 16 384) side measurement")
+    ap.add_argument("--no-qp50", action="store_true",
+                    help="skip the headline workload at acados' default QP cap (qp_solver_iter_max 50)")
     ap.add_argument("--no-closed-loop", action="store_true",
                     help="skip the closed-loop side measurement (main.m's loop over 16 384 lanes, SURVEY §8(f) row 1)")
     ap.add_argument("--nlp", choices=("SQP_RTI", "SQP"), default="SQP_RTI",
@@ -606,6 +610,7 @@ def main():
                        device=gpu, nlp_solver_type=args.nlp, factor_scan=args.factor_scan)
     solver.set_shapes([make_shape(n) for n in SHAPES])
     S_layout, L_layout = solver.layout()
+    factor_walk = solver.factor_walk()
     solver.set_stream_parts(args.stream_parts)
     parts = solver.stream_parts()
 
@@ -723,11 +728,8 @@ def main():
                    "nlp_solver_type": args.nlp,
                    "layout": {"stages_per_lane": S_layout, "lanes_per_instance": L_layout,
                               "stream_parts": parts, "factor_scan": bool(args.factor_scan and S_layout == 2),
-                              # the library's choice (qsp_solver.hip mfw_use): one stage per lane at
-                              # 15 <= N <= 31 factorises on the FP64 matrix cores
-                              "factor_walk": ("matrix cores (v_mfma_f64_4x4x4_4b_f64)"
-                                              if S_layout == 1 and 15 <= N <= 31 and os.environ.get("QSP_MFMA_WALK", "1") != "0"
-                                              else ("associative scan" if args.factor_scan and S_layout == 2 else "lane walk"))},
+                              # as the library reports it (qsp_get_factor_walk)
+                              "factor_walk": factor_walk},
                    "parallelism": f"dp{world} (contiguous lane shards, no collective in the solve)"},
         "kernel_ms_avg": avg_kern_s * 1e3,
         "qp_iters_mean_per_qp": float(qp_iter.mean() / K),
@@ -794,6 +796,35 @@ def main():
             result["host_boundary_u0_equals_device_u0"] = bool(np.array_equal(u_host, u0))
     solver.close()
 
+    if (rank == 0 and world == 1 and not cfg4 and args.nlp == "SQP_RTI" and not args.no_qp50
+            and args.qp_iters != 50):
+        # the same workload at acados' default QP cap, qp_solver_iter_max = 50, which the reference leaves
+        # in place (NMPC_controller.m:275): the same device-resident inputs and timing as the headline
+        s50 = OcpSolver(N=N, batch=Bl, sqp_iters=K, qp_iters=50, stages_per_lane=args.stages_per_lane,
+                        device=gpu, nlp_solver_type=args.nlp, factor_scan=args.factor_scan)
+        s50.set_shapes([make_shape(n) for n in SHAPES])
+        s50.set_stream_parts(args.stream_parts)
+        s50.solve_device(io, sh)
+        torch.cuda.synchronize(dev)
+        n50 = max(1, min(args.steps, 5))
+        t50 = time.perf_counter()
+        for _ in range(n50):
+            s50.solve_device(io, sh)
+        torch.cuda.synchronize(dev)
+        dt50 = time.perf_counter() - t50
+        s50.synchronize()
+        cap50 = s50.get("qp_capped")
+        it50 = s50.get("qp_iter")
+        u50 = d_u0.cpu().numpy()
+        result["configs2_qp50"] = {
+            "workload": "the headline workload with qp_iters_max = 50 (acados' qp_solver_iter_max default)",
+            "solves_per_s": Bl * n50 / dt50, "ratio_to_headline": Bl * n50 / dt50 / value,
+            "qp_capped_frac": float(cap50.sum() / (Bl * K)), "qp_iters_mean_per_qp": float(it50.mean() / K),
+            "status_nonzero_lanes": int(np.count_nonzero(d_st.cpu().numpy())),
+            "frac_u0_within_1e-6_of_cap20": float(np.mean(np.abs(u50 - u0).max(1) <= 1e-6)),
+            "steps": n50, "factor_walk": s50.factor_walk()}
+        s50.close()
+
     if rank == 0 and world == 1 and not args.no_configs1 and not cfg4:
         # BASELINE configs[1] beside the headline (its own GPU timing; CPU in full below)
         x1, traj1, sid1 = config1_inputs(N)
@@ -832,7 +863,8 @@ def main():
         result["configs4"] = {"workload": "BASELINE configs[4]: batch=16384, N=50, curved x_finals reference, random "
                                           "start index per lane, 4 shapes mixed per lane, K=50 SQP-RTI, cold start",
                               "gpu_solves_per_s": len(x4) * 3 / (time.perf_counter() - t4),
-                              "layout": {"stages_per_lane": S4, "lanes_per_instance": L4},
+                              "layout": {"stages_per_lane": S4, "lanes_per_instance": L4,
+                                         "factor_walk": s4.factor_walk()},
                               "note": "host-boundary controller solves (x0 in, u0 out), 3 repeats"}
         u4_gpu = s4.get_u0()
         # the factorisation-scan option (qsp_options.factor_scan) on the same workload: its rate, and its
@@ -851,7 +883,8 @@ def main():
         dsc = np.abs(u4_scan - u4_gpu).max(1)
         result["configs4"]["factor_scan"] = {"gpu_solves_per_s": len(x4) * 3 / (time.perf_counter() - t4s),
                                              "frac_u0_within_1e-6_of_default": float(np.mean(dsc <= 1e-6)),
-                                             "status_equal_lanes": int(np.sum(s4s.get("status") == s4.get("status")))}
+                                             "status_equal_lanes": int(np.sum(s4s.get("status") == s4.get("status"))),
+                                             "factor_walk": s4s.factor_walk()}
         s4s.close()
         # the GPU's own response to the literal parity leg's 1e-13 x0 probes (untimed)
         gpu_dev4 = np.zeros(len(x4))
@@ -871,14 +904,23 @@ def main():
         hc = host_cpu()
         threads = hc["threads"]
         nlp_mode = 1 if args.nlp == "SQP" else 0
-        # CPU baseline: the kernel-order twin (the same algorithm and formulation, OpenMP over lanes)
+        # CPU baseline: the twin in its fastest CPU order (the same algorithm and formulation, the
+        # factorisation as the lane walk's 4x4 algebra, OpenMP over lanes); the matrix-core order, which
+        # the CPU can only emulate, is timed beside it (it is the bit-exact checker below)
         n, dt, rt, run_t = cpu_baseline(x0, traj, sid, N, K, args.cpu_seconds, threads, nlp_mode, twin=True,
-                                        qp_iters=args.qp_iters)
+                                        qp_iters=args.qp_iters, lane_walk=1)
         result["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": threads, "kind": "port",
                                   "host_nproc": hc["nproc"], "host_affinity_cpus": hc["affinity_cpus"],
                                   "host_cgroup_cpu_quota": hc["cgroup_cpus"], "cpu_model": hc["model"],
                                   "sample": f"{n} lanes of the same workload (oracle/qsp_twin.c: the library's "
-                                            f"formulation on the CPU, OpenMP over {threads} threads, {dt:.1f} s)"}
+                                            f"formulation on the CPU, factorisation in the lane walk's order, OpenMP "
+                                            f"over {threads} threads, {dt:.1f} s)"}
+        nm, dtm, _, _ = cpu_baseline(x0, traj, sid, N, K, max(3.0, args.cpu_seconds / 3), threads, nlp_mode,
+                                     twin=True, qp_iters=args.qp_iters)
+        result["cpu_baseline"]["mfma_order_twin"] = {
+            "value": nm / dtm, "unit": "solves/s", "cores": threads,
+            "sample": f"{nm} lanes: the twin emulating the matrix cores' rounding order (the bit-exact checker; "
+                      "not the CPU's best formulation)"}
         result["cpu_baseline"]["thread_scaling"] = thread_scaling(run_t, n / dt, threads, hc["affinity_cpus"])
         # bit-exact parity: every lane of the batch against the twin (the CPU sample above included)
         from oracle.oracle import Oracle, make_opts

@@ -39,8 +39,8 @@ extern "C" {
 #define QSP_NY_E 4
 #define QSP_NH 3          /* h = [s; u_n; u_t]      (NMPC_controller.m:237) */
 #define QSP_MAX_CTRL 64   /* spline control points per shape */
-#define QSP_ABI_VERSION 3 /* 2: struct_size fields, qp_mu_max, qsp_get_qp_stalled, QP-failure exits;
-                             3: qsp_options.factor_scan */
+#define QSP_ABI_VERSION 4 /* 2: struct_size fields, qp_mu_max, qsp_get_qp_stalled, QP-failure exits;
+                             3: qsp_options.factor_scan; 4: qsp_get_factor_walk */
 
 #define QSP_OK 0
 #define QSP_ERR_ARG (-1)
@@ -149,6 +149,15 @@ int qsp_destroy(qsp_solver* s);
 const char* qsp_last_error(void);
 int qsp_version(void);                                 /* QSP_ABI_VERSION */
 int qsp_get_layout(const qsp_solver* s, int32_t* stages_per_lane, int32_t* lanes_per_instance);
+/* How the handle's QPs walk the horizon (the solver reports its own options, as acados' print does for
+ * ocp_opts, NMPC_controller.m:270-300).  The choice follows N, the layout and factor_scan, and it fixes
+ * the rounding order of every result: */
+#define QSP_WALK_LANE 0   /* the Riccati recursion as 4x4 algebra on one lane per stage, handed lane to lane */
+#define QSP_WALK_MFMA 1   /* on the FP64 matrix cores (v_mfma_f64_4x4x4_4b_f64, one instance per 16-lane
+                             block): the factorisation, and at one stage per lane (15 <= N <= 31) the
+                             closed-loop forward and difference walks too; two stages per lane: every N */
+#define QSP_WALK_SCAN 2   /* factor_scan = 1 at two stages per lane: the associative scan */
+int qsp_get_factor_walk(const qsp_solver* s, int32_t* walk);
 
 /* ------------------------------------------------------------- model / OCP */
 /* PLY contour -> ordered control points, knots, c_ellipse (PusherSliderModel.m:84-132, :53-55). */

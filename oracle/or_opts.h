@@ -58,6 +58,9 @@ typedef struct {
     int32_t probe_seed;
     int32_t factor_scan; /* twin only: at S = 2 the factorisation as the device's associative scan
                             (qsp_options.factor_scan) instead of the walk */
+    int32_t lane_walk;   /* twin only: 1 = factorise by the lane walk's order even where the device uses the
+                            matrix cores (the fastest CPU formulation of the same algorithm: bench.py's
+                            cpu_baseline; the matrix-core order, emulated, is the bit-exact checker) */
 } or_opts;
 
 #endif

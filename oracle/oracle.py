@@ -67,6 +67,7 @@ class Opts(C.Structure):
         ("qp_stall_alpha", C.c_double), ("qp_stall_iters", C.c_int32), ("stages_per_lane", C.c_int32),
         ("qp_mu_max", C.c_double),
         ("model_probe", C.c_double), ("probe_seed", C.c_int32), ("factor_scan", C.c_int32),
+        ("lane_walk", C.c_int32),
     ]
 
 
@@ -76,7 +77,7 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
               mu0=1.0, t_min=1e-2, frac=0.995, sigma_min=1e-2, mu_stop=1e-10, res_stop=1e-10, v_alpha=1.0, d_v=0.0, t_angle0=3.0,
               u_n_lb=0.0, u_t_ub=0.05, nlp_mode=0, tol=1e-6, ls_alpha_min=0.05, ls_alpha_red=0.7, ls_eps=1e-4,
               qp_tol_stat=1e-10, qp_tol_eq=1e-10, stage0_s_bound=1, qp_stall_alpha=1e-3, qp_stall_iters=3,
-              qp_mu_max=1e100, stages_per_lane=0, model_probe=0.0, probe_seed=0, factor_scan=0):
+              qp_mu_max=1e100, stages_per_lane=0, model_probe=0.0, probe_seed=0, factor_scan=0, lane_walk=0):
     o = Opts()
     o.N, o.sqp_iters, o.qp_iters, o.stage0_s_bound = N, sqp_iters, qp_iters, int(stage0_s_bound)
     o.qp_tol_stat, o.qp_tol_eq = qp_tol_stat, qp_tol_eq
@@ -84,6 +85,7 @@ def make_opts(N=20, sqp_iters=50, qp_iters=20, Ts=0.05, tau=None,
     o.qp_mu_max, o.stages_per_lane = qp_mu_max, int(stages_per_lane)
     o.model_probe, o.probe_seed = float(model_probe), int(probe_seed)
     o.factor_scan = int(factor_scan)
+    o.lane_walk = int(lane_walk)
     o.Ts = Ts
     o.tau = Ts if tau is None else tau
     o.W[:] = W

@@ -389,9 +389,9 @@ static void make_par(tw_par *p, const or_opts *o)
     const char *mw = getenv("QSP_MFMA_WALK");
     {
         const int G = 64 / p->L, H = (p->N + 1) / 2, CM = p->N + 1 - H;
-        const int cap = (p->S == 1 ? 12 + 2 : 24 + 3) * 64;   /* F_VA .. F_HG per slot + mfw_extra, x 64 lanes */
-        const int fits = G <= 4 && G * CM * 27 <= cap && (p->S == 2 || (p->N >= 15 && p->N <= 31));
-        p->mfma_walk = fits && !(mw && mw[0] == '0');
+        const int cap = (p->S == 1 ? 12 + 2 : 24 + 4) * 64;   /* F_VA .. F_HG per slot + mfw_extra, x 64 lanes */
+        const int fits = G <= 4 && G * CM * 27 + 5 <= cap && (p->S == 2 || (p->N >= 15 && p->N <= 31));   /* + 5 constants */
+        p->mfma_walk = fits && !(mw && mw[0] == '0') && !o->lane_walk;
     }
     p->Ts = o->Ts;
     p->tau = o->tau;

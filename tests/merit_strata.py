@@ -87,3 +87,46 @@ def check_step(u, status, iters, ref, stable, far, what):
         assert np.mean(status[edge] == ref["status"][edge]) >= 0.92, (what, np.mean(status[edge] == ref["status"][edge]))
         assert np.mean(iters[edge] == ref["iters"][edge]) >= 0.90, (what, np.mean(iters[edge] == ref["iters"][edge]))
     return {"stable": int(stable.sum()), "far": int(far.sum()), "edge": int(edge.sum())}
+
+
+def classify_order_flips(lit, op, x0, sid, traj, flips, probes=(1e-13, -1e-13, 3e-13)):
+    """Lanes whose status differs between two rounding orders of the same solver (e.g. the twin with the
+    matrix-core and with the lane-walk factorisation order): for each, whether the literal restatement,
+    run with the controller_pair protocol (the same x0, index_time 1 then 2, warm-started), puts it on a
+    decision edge (a KKT test within KKT_DECADES of tol or an Armijo test within ARMIJO_REL, at any step
+    up to the one given) or moves its u0 (> 1e-9), status or sqp_iter under relative x0 probes at that
+    step (rounding-chaotic).  flips: (lane, step) pairs, step 0 or 1.  Returns one dict per flip; a flip
+    with neither is a far-stratum lane, where two orders of the same arithmetic must agree."""
+    import ctypes as C
+    lanes = np.array(sorted({int(i) for i, _ in flips}), dtype=np.int64)
+    nb, N = len(lanes), op.N
+    if nb == 0:
+        return []
+
+    def run(f, diag=None):
+        warm = lit.new_warm(nb, N)
+        out = []
+        for step in range(2):
+            if diag is not None:
+                lit.L.or_set_kkt_diag(diag[step].ctypes.data_as(C.c_void_p))
+            try:
+                out.append(lit.controller_solve(op, x0[lanes] * (1 + f), traj, 1 + step, warm, shape_id=sid[lanes]))
+            finally:
+                lit.L.or_set_kkt_diag(None)
+        return out
+    diag = [np.zeros((nb, KKT_DIAG)), np.zeros((nb, KKT_DIAG))]
+    base = run(0.0, diag)
+    moves = [np.zeros(nb, bool), np.zeros(nb, bool)]
+    for f in probes:
+        p = run(f)
+        for step in range(2):
+            moves[step] |= ((p[step]["status"] != base[step]["status"]) | (p[step]["iters"] != base[step]["iters"])
+                            | (np.abs(p[step]["u0"] - base[step]["u0"]).max(1) > 1e-9))
+    out = []
+    for i, step in flips:
+        j = int(np.searchsorted(lanes, i))
+        km = min(diag[s][j, 18] for s in range(step + 1))
+        am = min(diag[s][j, 20] for s in range(step + 1))
+        out.append({"lane": int(i), "step": int(step), "kkt_margin": float(km), "armijo_margin": float(am),
+                    "edge": bool(km <= KKT_DECADES or am <= ARMIJO_REL), "chaotic": bool(moves[step][j])})
+    return out

@@ -279,3 +279,34 @@ def test_horizon_and_layout_edges(oracle, N, S):
     # solution: 4e-9 seen there, held to 1e-8
     np.testing.assert_allclose(X[ok], w["X"].reshape(nb, N + 1, 4)[ok], rtol=0, atol=1e-9 if N <= 90 else 1e-8)
     np.testing.assert_allclose(u[~ok], r["u0"][~ok], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("N, kw, want", [
+    (14, {}, "lane walk"),                                        # five instances per wave: no block each
+    (15, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),
+    (20, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),          # the headline
+    (31, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),
+    (50, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),          # configs[4]: two stages per lane
+    (50, {"factor_scan": True}, "associative scan"),
+    (20, {"stages_per_lane": 2}, "lane walk"),                   # 11 lanes: five instances per wave
+])
+def test_library_reports_its_factor_walk(N, kw, want):
+    """qsp_get_factor_walk (ABI 4) reports the walk the launchers take, so bench lines label runs by what
+    ran (qsp_solver.hip factor_walk_kind = mfw_use / factor_scan)."""
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    s = OcpSolver(N=N, batch=8, **kw)
+    try:
+        assert s.factor_walk() == want
+    finally:
+        s.close()
+
+
+def test_lane_walk_switch_is_reported(monkeypatch):
+    from uclv_qs_pushing_matlab_amd.solver import OcpSolver
+    monkeypatch.setenv("QSP_MFMA_WALK", "0")
+    for N in (20, 50):
+        s = OcpSolver(N=N, batch=8)
+        try:
+            assert s.factor_walk() == "lane walk"
+        finally:
+            s.close()

@@ -181,6 +181,20 @@ def test_merit_sqp_bit_identical(twin):
     # multiplier update; exact QP duals do not change it -- is DESIGN.md section 2's residual breakdown
     # (tests/test_merit_diagnosis.py pins it on the literal oracle).
     assert int(np.sum(r["status"] == 0)) == 1010
+    # the count depends on the factorisation's rounding order (1 004 with the lane walk's): every lane
+    # whose status the order decides sits outside the far stratum of the literal restatement -- on a
+    # KKT/Armijo decision edge or rounding-chaotic under 1e-13 x0 probes (tests/merit_strata.py,
+    # tests/test_merit_diagnosis.py::test_factor_order_flips_lie_outside_the_far_stratum)
+    from merit_strata import classify_order_flips
+    from oracle.oracle import Oracle, make_opts
+    opl = make_opts(N=20, sqp_iters=30, nlp_mode=1, qp_iters=20, lane_walk=1)
+    warm = twin.new_warm(4096, 20)
+    lw = [twin.controller_solve(opl, x0, traj, 1 + k, warm, shape_id=sid)["status"] for k in range(2)]
+    assert int(np.sum(lw[1] == 0)) == 1004
+    flips = [(int(i), 1) for i in np.flatnonzero(lw[1] != r["status"])]
+    cls = classify_order_flips(Oracle(NAMES), make_opts(N=20, sqp_iters=30, nlp_mode=1, qp_iters=20), x0, sid, traj,
+                               flips)
+    assert len(cls) == 8 and all(c["edge"] or c["chaotic"] for c in cls), cls
     assert set(np.unique(r["status"])) <= {0, 2}
     st2 = r["status"] == 2
     assert np.mean(r["kkt"][st2, :3].max(1) >= 1e-6) > 0.95   # stationarity fails on the status-2 lanes

@@ -199,6 +199,35 @@ def test_mfma_walk_matches_lane_walk(twin, monkeypatch):
         assert np.median(err["1"]) < 2 * np.median(err["0"]) + 1e-15, (N, np.median(err["1"]), np.median(err["0"]))
 
 
+def test_mfma_walk_matches_lane_walk_two_stages_per_lane(twin):
+    """The same check at two stages per lane (N + 1 > 32: configs[4]'s layout), where the matrix-core
+    factorisation is also the default (round 5): N = 32, 50 and 127, three SQP-RTI iterations of 64 lanes
+    against the literal formulas in __float128, the twin in the device's matrix-core order and in the lane
+    walk's (or_opts.lane_walk).  Measured: lanes beyond 1e-9 of quad 6 / 8 / 5 (matrix cores), 5 / 8 / 4
+    (lane walk), 5 / 9 / 6 (the double literal); medians 3.1e-13 / 1.0e-13 / 4.3e-13 against 2.6e-13 /
+    9.2e-14 / 6.9e-13; the largest error smaller with the matrix cores at every horizon (6.9e-6 / 1.8e-4 /
+    2.5e-4 against 1.2e-5 / 5.5e-4 / 1.6e-3)."""
+    nb = 64
+    x0 = config2_x0(nb, 13)
+    sid = np.arange(nb) % 4
+    traj = straight_traj()
+    lit = Oracle(NAMES)
+    for N in (32, 50, 127):
+        op = make_opts(N=N, sqp_iters=3)
+        q = lit.controller_solve_ext(op, x0, traj, 1, lit.new_warm(nb, N), shape_id=sid, precision="quad")["u0"]
+        dl = np.abs(lit.controller_solve(op, x0, traj, 1, lit.new_warm(nb, N), shape_id=sid)["u0"] - q).max(1)
+        err = {}
+        for lw in (0, 1):
+            u = twin.controller_solve(make_opts(N=N, sqp_iters=3, lane_walk=lw), x0, traj, 1, twin.new_warm(nb, N),
+                                      shape_id=sid)["u0"]
+            err[lw] = np.abs(u - q).max(1)
+        assert not np.array_equal(err[0], err[1]), f"N={N}: the two walks should round differently"
+        far = [int(np.sum(e > 1e-9)) for e in (err[0], err[1], dl)]
+        assert max(far) - min(far) <= 2, (N, far)
+        assert np.median(err[0]) < 2 * np.median(err[1]) + 1e-15, (N, np.median(err[0]), np.median(err[1]))
+        assert err[0].max() <= 2 * err[1].max(), (N, err[0].max(), err[1].max())
+
+
 def test_s2_scans_across_horizons(twin):
     """The S = 2 layout's scans (forward and corrector-difference passes as Hillis-Steele scans over
     the group's lanes, at any lane count L = ceil((N+1)/2), powers of two or not) against the S = 1

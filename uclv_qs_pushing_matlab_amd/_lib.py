@@ -12,7 +12,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 # QSP_LIB_PATH: developer override (A/B runs of differently compiled libraries)
 LIB_PATH = os.environ.get("QSP_LIB_PATH") or os.path.join(_PKG, "libqsp_nmpc.so")
 MAX_CTRL = 64
-ABI_VERSION = 3   # include/qsp_nmpc.h QSP_ABI_VERSION
+ABI_VERSION = 4   # include/qsp_nmpc.h QSP_ABI_VERSION
 
 _lib = None
 
@@ -72,6 +72,7 @@ _SIGS = {
     "qsp_destroy": [_P],
     "qsp_version": [],
     "qsp_get_layout": [_P, C.POINTER(_I), C.POINTER(_I)],
+    "qsp_get_factor_walk": [_P, C.POINTER(_I)],
     "qsp_shape_from_ply": [C.c_char_p, _I, _D, _D, _D, _D, C.POINTER(Shape)],
     "qsp_set_shapes": [_P, C.POINTER(Shape), _I],
     "qsp_set_shape_ids": [_P, _P],

@@ -500,6 +500,12 @@ int qsp_get_layout(const qsp_solver* s, int32_t* S, int32_t* L) {
     return QSP_OK;
 }
 
+int qsp_get_factor_walk(const qsp_solver* s, int32_t* walk) {
+    if (!s || !walk) return fail(QSP_ERR_ARG, "qsp_get_factor_walk: null argument");
+    *walk = factor_walk_kind(s->p, s->S);
+    return QSP_OK;
+}
+
 // ------------------------------------------------------------------ shapes
 int qsp_shape_from_ply(const char* path, int32_t flip, double mu_sg, double mu_sp, double mass, double tau_max,
                        qsp_shape* out) {

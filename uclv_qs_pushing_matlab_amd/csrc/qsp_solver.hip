@@ -43,6 +43,28 @@
 
 namespace qsp {
 
+// Diagnostic build only (-DQSP_SEGSTAMP, scripts/segstamps.py): wave cycles per QP-kernel segment, summed
+// over the waves by lane 0 of each (s_memtime; the stamps themselves cost ~10 % of the wave time).
+#ifdef QSP_SEGSTAMP
+#ifndef QSP_SEGMASK
+#define QSP_SEGMASK 0xffffffffu   // which segments are stamped (fewer stamps: less distortion)
+#endif
+__device__ unsigned long long g_seg[32];
+__device__ __forceinline__ unsigned long long seg_now() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void seg_add(int i, unsigned long long t0) {
+    if (!((QSP_SEGMASK >> i) & 1u)) return;
+    const unsigned long long t = seg_now();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_seg[i], t - t0);
+}
+#define SEG_T(v) unsigned long long v = seg_now()
+#define SEG_ADD(i, v) seg_add(i, v)
+#define SEG_NEXT(i, v) do { seg_add(i, v); v = seg_now(); } while (0)
+#else
+#define SEG_T(v)
+#define SEG_ADD(i, v)
+#define SEG_NEXT(i, v)
+#endif
+
 // ------------------------------------------------------------- group helpers
 // Reductions over the L lanes of an instance group (lanes base .. base+L-1), leaving the
 // same value in every lane of the group (identical decisions in all lanes of an instance).
@@ -169,7 +191,7 @@ enum LdsField : int {
 // (S = 1: two, so eight one-wave workgroups and a packing-sort workgroup still share a CU's LDS; S = 2:
 // three, every horizon up to N = 127)
 template <int S>
-constexpr int mfw_extra() { return S == 1 ? 2 : 3; }
+constexpr int mfw_extra() { return S == 1 ? 2 : 4; }
 template <int S>
 constexpr int lds_bytes() { return (F_COUNT * S + mfw_extra<S>()) * BLOCK * 8; }
 
@@ -393,11 +415,22 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 // phases (stages H .. N-1 with the terminal record, then 0 .. H-1).
 enum MfwSlot : int { R_A = 0, R_B = 6, R_BB = 14, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
 enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 of Z = [R~ | r~ | .]
-static_assert((F_COUNT - F_VA + mfw_extra<1>()) * BLOCK >= 33 * MFW_REC, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
-static_assert(((F_COUNT - F_VA) * 2 + mfw_extra<2>()) * BLOCK >= 64 * MFW_REC, "S = 2: records of G (N/2 + 1) stages, N <= 127");
+// the operand constants (A's ones and zeros, the zero column of [B | b | 0], Hx's fixed diagonal), at the
+// end of the region: the lanes whose operand element is one read it there instead of from the record
+enum MfwConst : int { C_ONE = 0, C_ZERO = 1, C_HX = 2, C_COUNT = 5 };
+static_assert((F_COUNT - F_VA + mfw_extra<1>()) * BLOCK >= 33 * MFW_REC + C_COUNT, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
+static_assert(((F_COUNT - F_VA) * 2 + mfw_extra<2>()) * BLOCK >= 64 * MFW_REC + C_COUNT, "S = 2: records of G (N/2 + 1) stages, N <= 127");
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {   // a'b + c per 4x4 block
     return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+// The walk hands data between lanes of the one wave through LDS (stage lanes publish, block lanes read,
+// and back).  LDS executes a wave's instructions in order; this makes the order explicit to the compiler
+// (no instruction on a single wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 template <int CTRL>
 __device__ __forceinline__ double quad_bcast(double v) {   // DPP quad_perm: one lane of each quad to all four
@@ -416,7 +449,7 @@ constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + mfw_extra<S>()) * BL
 __host__ __device__ __forceinline__ bool mfw_fits(int N, int S) {
     const int L = (N + S) / S, G = 64 / L, H = (N + 1) / 2, CM = N + 1 - H;
     const int cap = S == 1 ? mfw_region<1>() : mfw_region<2>();
-    return G <= 4 && G * CM * MFW_REC <= cap && (S == 2 || (N >= 15 && N <= 31));
+    return G <= 4 && G * CM * MFW_REC + C_COUNT <= cap && (S == 2 || (N >= 15 && N <= 31));
 }
 __host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p, int S) {
     return p.mfma_walk != 0 && mfw_fits(p.N, S);
@@ -436,17 +469,20 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     const int b = (l >> 2) & 3, r = l >> 4, cc = l & 3;
     const int bg = b < G ? b : G - 1;
     const bool wr = b < G;
+    // each operand element's record slot (-1: a structural constant, read from the constant slots instead)
     int ao = -1;
     if (cc >= 2 && r < 2) ao = R_A + 2 * r + (cc - 2);
     else if (cc == 3 && r >= 2) ao = R_A + 2 + r;
-    const double aconst = r == cc ? 1.0 : 0.0;
     const int go = cc < 2 ? R_B + 2 * r + cc : (cc == 2 ? R_BB + r : -1);
-    int xo = -1;   // the C operand of Q (Hx: only hx3 varies) and of Z (Hu, gu) share one read
-    if (r == 3 && cc == 3) xo = R_HX3;
-    else if (r < 2 && r == cc) xo = R_HU + r;
-    else if (r < 2 && cc == 2) xo = R_GU + r;
-    const double hxc = r == 0 ? p.tau * p.W[0] : (r == 1 ? p.tau * p.W[1] : p.tau * p.W[2]);
-    const int ao_ = ao < 0 ? 0 : ao, go_ = go < 0 ? 0 : go, xo_ = xo < 0 ? 0 : xo;
+    const int ho = (r == 3 && cc == 3) ? R_HX3 : -1;   // Q's C (Hx): only hx3 varies
+    int zo = -1;                                       // Z's C: Hu on the diagonal, gu in column 2
+    if (r < 2 && r == cc) zo = R_HU + r;
+    else if (r < 2 && cc == 2) zo = R_GU + r;
+    const int qo = cc == 2 ? R_GX + r : -1;            // q~'s C: gx in column 2 (p lives there only)
+    double* const cst = reg + mfw_region<S>() - C_COUNT;
+    const int ac = r == cc ? C_ONE : C_ZERO, hc = r == cc && r < 3 ? C_HX + r : C_ZERO;
+    if (c.lane < C_COUNT)   // the constants (the region's other fields change between walks)
+        cst[c.lane] = c.lane == C_ONE ? 1.0 : (c.lane == C_ZERO ? 0.0 : p.tau * p.W[c.lane < C_HX ? 0 : c.lane - C_HX]);
     double P = 0.0, pv = 0.0;
     for (int ph = 0; ph < 2; ++ph) {
         const int kb = ph == 0 ? H : 0, ke = ph == 0 ? N : H - 1;   // records kb .. ke
@@ -503,40 +539,31 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                 }
             }
         }
+        wave_lds_sync();
         const double* rb = reg + bg * CM * MFW_REC;   // this block's records of the phase
         if (ph == 0) {
             P = r == cc ? (r == 0 ? p.We[0] : (r == 1 ? p.We[1] : (r == 2 ? p.We[2] : p.We[3]))) : 0.0;
-            pv = rb[(N - kb) * MFW_REC + R_GX + r];
+            pv = cc == 2 ? rb[(N - kb) * MFW_REC + R_GX + r] : 0.0;   // p_N = g_N (column 2)
         }
         const int kf = ph == 0 ? N - 1 : H - 1;
-        double va = rb[(kf - kb) * MFW_REC + ao_], vg = rb[(kf - kb) * MFW_REC + go_];
-        double vx = rb[(kf - kb) * MFW_REC + xo_], vq = rb[(kf - kb) * MFW_REC + R_GX + r];
-        for (int k = kf; k >= kb; --k) {
+        // one step of the walk from its operand elements (Am: A, G2: [B | b | 0], CH and CZ: the C operands
+        // of Q and Z, gq: gx); p lives in column 2 of pv, zero in the others, so T2 takes it as its C operand
+        auto step = [&](int k, double Am, double G2, double CH, double CZ, double gq) {
             double* rk = reg + (bg * CM + (k - kb)) * MFW_REC;
-            const double Am = ao >= 0 ? va : aconst;
-            const double G2 = go >= 0 ? vg : 0.0;
-            const double CH = r == cc ? (r == 3 ? vx : hxc) : 0.0;
-            const double CZ = xo >= 0 && r < 2 ? vx : 0.0;
-            const double gq = vq;
-            if (k > kb) {   // the next step's operand elements
-                const double* rn = rk - MFW_REC;
-                va = rn[ao_]; vg = rn[go_]; vx = rn[xo_]; vq = rn[R_GX + r];
-            }
             const double T1 = mfma4(P, Am, 0.0);                    // P'A
-            const double T2 = mfma4(P, G2, cc == 2 ? pv : 0.0);     // P'[B | b | 0] + [0 | 0 | p | 0]
+            const double T2 = mfma4(P, G2, pv);                     // P'[B | b | 0] + [0 | 0 | p | 0]
             const double Y = mfma4(G2, T1, 0.0);                    // rows 0, 1: S~ = B'P'A
             const double Z = mfma4(G2, T2, CZ);                     // rows 0, 1: [R~ | r~]
             const double Q = mfma4(Am, T1, CH);                     // Hx + A'P'A
             const double Qt = mfma4(T1, Am, CH);                    // its transpose (below)
-            const double pp = quad_bcast<0xAA>(T2);                 // (p + P'b)[r] across the row
-            const double qv = mfma4(Am, pp, gq);                    // q~ = gx + A'pp (across the row)
-            // R~ and r~ on the lanes of rows 0 and 1: v_permlane16_swap puts row 0 of Z into rows 0, 1
-            // of its first result and row 1 into rows 0, 1 of the second; quad broadcasts pick columns
+            const double pp = cc == 2 ? T2 : 0.0;                   // p + P'b (column 2)
+            const double qv = mfma4(Am, pp, gq);                    // q~ = gx + A'pp (column 2; the others +0)
+            // R~ on the lanes of rows 0 and 1: v_permlane16_swap puts row 0 of Z into rows 0, 1 of its
+            // first result and row 1 into rows 0, 1 of the second; quad broadcasts pick columns
             const auto slo = __builtin_amdgcn_permlane16_swap(__double2loint(Z), __double2loint(Z), false, false);
             const auto shi = __builtin_amdgcn_permlane16_swap(__double2hiint(Z), __double2hiint(Z), false, false);
             const double w0 = __hiloint2double(shi[0], slo[0]), w1 = __hiloint2double(shi[1], slo[1]);
-            const double R00 = quad_bcast<0x00>(w0), R01 = quad_bcast<0x55>(w0), rt0 = quad_bcast<0xAA>(w0);
-            const double R11 = quad_bcast<0x55>(w1), rt1 = quad_bcast<0xAA>(w1);
+            const double R00 = quad_bcast<0x00>(w0), R01 = quad_bcast<0x55>(w0), R11 = quad_bcast<0x55>(w1);
             // K = -R~^-1 S~ = (Xa'S~) / det with Xa = -adj R~: the product does not wait for the reciprocal
             const double det = qfma(R00, R11, -(R01 * R01));
             const double Xa = (r < 2 && cc < 2) ? (r != cc ? R01 : (r == 0 ? -R11 : -R00)) : 0.0;
@@ -554,13 +581,36 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                 // (K'S~ + Q~', Q~' = T1'A + Hx: the same products in the same order, so bit for bit the
                 // transpose): a symmetric P as the lane walk's.  Left to drift apart, the two triangles
                 // cost the ill-conditioned QPs up to 1e3x the walk's error (tests/test_gpu_parity.py).
-                const double RT = r == 0 ? rt0 : (r == 1 ? rt1 : 0.0);
+                const double RT = r < 2 && cc == 2 ? Z : 0.0;       // r~ (column 2)
                 const double Pu = mfma4(Y, Kf, Q);                  // Q~ + S~'K
                 const double Pl = mfma4(Kf, Y, Qt);                 // its transpose
                 P = r <= cc ? Pu : Pl;
-                pv = mfma4(Kf, RT, qv);                             // q~ + K'r~
+                pv = mfma4(Kf, RT, qv);                             // q~ + K'r~ (column 2; the others +0)
             }
+        };
+        // two operand sets, each read one step ahead, so the prefetch never waits on the step it feeds.
+        // A lane reads each operand element through its own pointer: a record slot, stepping one record
+        // down per step, or a constant slot, standing still (stride 0) -- no per-step selects
+        const double* r0 = rb + (kf - kb) * MFW_REC;
+        const double *pa = ao >= 0 ? r0 + ao : cst + ac, *pg = go >= 0 ? r0 + go : cst + C_ZERO;
+        const double *ph_ = ho >= 0 ? r0 + ho : cst + hc, *pz = zo >= 0 ? r0 + zo : cst + C_ZERO;
+        const double* pq = qo >= 0 ? r0 + qo : cst + C_ZERO;
+        const int sa = ao >= 0 ? MFW_REC : 0, sg = go >= 0 ? MFW_REC : 0, sh = ho >= 0 ? MFW_REC : 0;
+        const int sz = zo >= 0 ? MFW_REC : 0, sq = qo >= 0 ? MFW_REC : 0;
+        double aA = *pa, gA = *pg, hA = *ph_, zA = *pz, qA = *pq, aB = 0.0, gB = 0.0, hB = 0.0, zB = 0.0, qB = 0.0;
+        pa -= sa; pg -= sg; ph_ -= sh; pz -= sz; pq -= sq;
+        // (the reads one record past the phase's last stage land inside the workgroup's LDS and go unused)
+        for (int k = kf;; k -= 2) {
+            aB = *pa; gB = *pg; hB = *ph_; zB = *pz; qB = *pq;
+            pa -= sa; pg -= sg; ph_ -= sh; pz -= sz; pq -= sq;
+            step(k, aA, gA, hA, zA, qA);
+            if (k == kb) break;
+            aA = *pa; gA = *pg; hA = *ph_; zA = *pz; qA = *pq;
+            pa -= sa; pg -= sg; ph_ -= sh; pz -= sz; pq -= sq;
+            step(k - 1, aB, gB, hB, zB, qB);
+            if (k - 1 == kb) break;
         }
+        wave_lds_sync();
         // collect: the stage lanes take their slots' factors (stages k < N)
         if constexpr (S == 1) {
             if (c.grp < G && c.lig >= kb && c.lig <= ke && c.lig < N) {
@@ -595,6 +645,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                 }
             }
         }
+        wave_lds_sync();   // the next phase's records overwrite these
     }
     // the overlaid fields read later: the terminal and padding slots' F_VA / F_VN stay zero (the
     // forward passes write them on the stages k < N only; qp_ipm's start defines them)
@@ -961,6 +1012,7 @@ __device__ __forceinline__ void apply_step(const Stage<S>& st, int ls, const dou
 template <int S, bool FACTOR, bool ALT = false>
 __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4],
                                               int out, double (&M)[S][16]) {
+    SEG_T(t_rs);
     double P[10], pv[4];
 #pragma unroll
     for (int i = 0; i < 10; ++i) P[i] = 0.0;
@@ -1169,6 +1221,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
         }
     }
     }
+    SEG_NEXT(FACTOR ? 2 : 6, t_rs);
     if constexpr (S == 1) {
         // forward in closed-loop form: dx_{k+1} = (A + B K) dx_k + (B kk + b), so a step is
         // one 4x4 affine map (16 FMA) instead of du = kk + K dx followed by the dynamics;
@@ -1209,6 +1262,7 @@ __device__ __forceinline__ void riccati_solve(const Ctx& c, const SolveParams& p
             st.f(out, 0, 1) = qfma(K[3], dxk[3], qfma(K[2], dxk[2], qfma(K[1], dxk[1], qfma(K[0], dxk[0], st.kk[0][0]))));
             st.f(out, 0, 2) = qfma(K[7], dxk[3], qfma(K[6], dxk[2], qfma(K[5], dxk[1], qfma(K[4], dxk[0], st.kk[0][1]))));
         }
+        SEG_ADD(FACTOR ? 3 : 7, t_rs);
         return;
     }
     if constexpr (S == 2) {
@@ -1299,6 +1353,7 @@ enum QpExit : int { QP_EXIT_CONV = 0, QP_EXIT_CAP = 1, QP_EXIT_STALL = 2, QP_EXI
 template <int S, bool ALT = false>
 __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const double dx0[4], int& exit,
                       bool skip = false) {
+    SEG_T(t_ipm);
     const double m = 2.0 * (3.0 * c.N - (p.s0_bound ? 0.0 : 1.0));
     // initial point.  r0 = largest bound residual of the infeasible start (t - d where the
     // slack had to be floored at t_min); every update scales all residuals by (1 - alpha)
@@ -1353,7 +1408,9 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
     double rscale = 1.0;
     int nit = 0, stall = 0;
     bool conv = false, stalled = false, div = false;
+    SEG_ADD(13, t_ipm);
     for (int it = 0;; ++it) {
+        SEG_T(t_seg);
         double tl_sum = 0.0;
 #pragma unroll
         for (int ls = 0; ls < S; ++ls)
@@ -1370,11 +1427,17 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         // the cap is tested after the last step too (conv reports it), then the loop ends
         if (it == p.qp_iters || __ballot(!done) == 0ull) break;
         nit += done ? 0 : 1;
+#ifdef QSP_SEGSTAMP
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_seg[31], 1ull);
+#endif
+        SEG_NEXT(0, t_seg);
         // ---- predictor
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) barrier_terms<S>(c, p, st, ls);
+        SEG_NEXT(1, t_seg);
         double M[S][16];   // closed-loop matrices A + B K (S = 1), shared by both forward walks
         riccati_solve<S, true, ALT>(c, p, st, dx0, F_VA, M);
+        SEG_T(t_seg2);
         // affine directions: computed once, kept in registers through the corrector
         double at[S][6], al[S][6];
         double num = 1.0, den = 1.0;
@@ -1388,10 +1451,13 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
         const double r = mua / mu;
         const double sg = fmax(r * r * r, p.sigma_min);
         const double smu = sg * mu;
+        SEG_NEXT(4, t_seg2);
         // ---- corrector
 #pragma unroll
         for (int ls = 0; ls < S; ++ls) corrector_terms<S>(c, p, st, ls, at[ls], al[ls], smu);
+        SEG_ADD(5, t_seg2);
         riccati_solve<S, false, ALT>(c, p, st, dx0, F_VN, M);
+        SEG_T(t_seg3);
         double dt[S][6], dl[S][6];
         num = 1.0; den = p.frac;       // initial bound 1/frac
 #pragma unroll
@@ -1409,6 +1475,7 @@ __device__ int qp_ipm(const Ctx& c, const SolveParams& p, Stage<S>& st, const do
                 st.du(ls, 1) = qfma(alpha, st.f(F_VN, ls, 2) - st.du(ls, 1), st.du(ls, 1));
             }
         }
+        SEG_ADD(8, t_seg3);
     }
     exit = conv ? QP_EXIT_CONV : (div ? QP_EXIT_DIVERGED : (stalled ? QP_EXIT_STALL : QP_EXIT_CAP));
     return nit;
@@ -1742,6 +1809,7 @@ __device__ __forceinline__ bool qp_outcome(const SolveArgs& A, const Ctx& c, con
 
 template <int S, bool MERIT = false, bool LIN = false, bool ALT = false>
 __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs A, int it) {
+    SEG_T(t_k);
     extern __shared__ double smem[];
     const SolveParams& p = A.p;
     Ctx c;
@@ -1765,7 +1833,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
     Stage<S> st;
     st.lds = smem + threadIdx.x;
     if (A.flags & QSP_FLAG_POISON) {
-        for (int f = 0; f < F_COUNT * S; ++f) st.lds[f * BLOCK] = __builtin_nan("");
+        for (int f = 0; f < F_COUNT * S + mfw_extra<S>(); ++f) st.lds[f * BLOCK] = __builtin_nan("");
     }
     double* X = A.wX + (size_t)iv * (N + 1) * 4;
     double* U = A.wU + (size_t)iv * N * 2;
@@ -1852,7 +1920,9 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
     }
     int exit;
+    SEG_NEXT(10, t_k);
     const int nit = qp_ipm<S, ALT>(c, p, st, dx0, exit, skip);
+    SEG_NEXT(11, t_k);
     qp_rollout<S>(c, st, dx0);
     const bool failed = qp_outcome<S>(A, c, st, iv, it, exit, skip);
     if (A.wnit && c.real && c.lig == 0) {
@@ -1919,6 +1989,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
         }
         if (k == 0) A.qp_iter[iv] += nit;
     }
+    SEG_ADD(12, t_k);
 }
 
 // Small batches (fewer waves than the chip's 2 048 wave slots), nlp_mode 0: the whole SQP loop
@@ -1933,7 +2004,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
     const SolveParams& p = A.p;
     const int N = p.N;
     if (A.flags & QSP_FLAG_POISON) {
-        for (int f = 0; f < F_COUNT * S; ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
+        for (int f = 0; f < F_COUNT * S + mfw_extra<S>(); ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
     }
     bool stopped = false;   // group-uniform: a failed QP stops the instance's SQP
     for (int it = 0; it < p.sqp_iters; ++it) {
@@ -1941,7 +2012,7 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) sqp_loop_kernel(SolveArg
         // debug: re-poisoned at every SQP iteration, so a read of a word the current iteration
         // did not write shows up (the last iteration's finite values would hide it)
         if (it > 0 && (A.flags & QSP_FLAG_POISON)) {
-            for (int f = 0; f < F_COUNT * S; ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
+            for (int f = 0; f < F_COUNT * S + mfw_extra<S>(); ++f) smem[threadIdx.x + f * BLOCK] = __builtin_nan("");
         }
         // lane geometry and addresses re-derived every iteration from an opaque lane id: hoisted
         // out of the loop they would stay live through the interior point (register budget)
@@ -2626,6 +2697,23 @@ static hipError_t launch_qp_any(const SolveArgs& a, int S, int it, hipStream_t s
 }
 
 int lanes_per_instance(int N, int S) { return (N + S) / S; }
+
+#ifdef QSP_SEGSTAMP
+// diagnostic build: read (and optionally clear) the segment cycle sums
+extern "C" int qsp_debug_segments(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg), sizeof(g_seg)) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned long long zero[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
+int factor_walk_kind(const SolveParams& p, int S) {
+    if (S == 2 && p.factor_scan) return QSP_WALK_SCAN;
+    return (S == 1 || S == 2) && mfw_use(p, S) ? QSP_WALK_MFMA : QSP_WALK_LANE;
+}
 
 static hipError_t launch_sqp_merit(const SolveArgs& a, int it, hipStream_t stream) {
     const int L = a.p.N + 1;

@@ -97,6 +97,14 @@ class OcpSolver:
         check(self._L.qsp_get_layout(self._h, C.byref(S), C.byref(L)), "qsp_get_layout")
         return S.value, L.value
 
+    FACTOR_WALKS = {0: "lane walk", 1: "matrix cores (v_mfma_f64_4x4x4_4b_f64)", 2: "associative scan"}
+
+    def factor_walk(self):
+        """How the QPs walk the horizon, as the library reports it (qsp_get_factor_walk, QSP_WALK_*)."""
+        w = C.c_int32()
+        check(self._L.qsp_get_factor_walk(self._h, C.byref(w)), "qsp_get_factor_walk")
+        return self.FACTOR_WALKS[w.value]
+
     # --------------------------------------------------------------- model
     def set_shapes(self, shapes, shape_id=None):
         arr = (_lib.Shape * len(shapes))(*shapes)
