@@ -292,9 +292,10 @@ int qsp_synchronize(qsp_solver* s);
  * counterpart (an execution choice of the batched engine).  get: the count the next solve uses.
  * Batches whose waves fit the GPU's SIMDs once (nlp_mode 0) run the whole SQP loop in one launch
  * instead (one part; environment QSP_FUSED_LOOP=0/1 at qsp_create overrides the automatic choice).
- * At one stage per lane and 15 <= N <= 31 the Riccati factorisation runs on the FP64 matrix cores
- * (DESIGN.md section 4); environment QSP_MFMA_WALK=0 at qsp_create selects the lane walk instead, a
- * developer A/B that rounds differently (the oracle twin follows the same variable). */
+ * The Riccati factorisation runs on the FP64 matrix cores at one stage per lane for 15 <= N <= 31 and at
+ * two stages per lane for every N (qsp_get_factor_walk reports it); environment
+ * QSP_MFMA_WALK=0 at qsp_create selects the lane walk instead, a developer A/B that rounds differently
+ * (the oracle twin follows the same variable). */
 int qsp_set_stream_parts(qsp_solver* s, int32_t parts);
 int qsp_get_stream_parts(qsp_solver* s, int32_t* parts);
 /* Per-kernel timing (acados' time_lin / time_qp split).  qsp_set_kernel_timing(s, n) pre-creates

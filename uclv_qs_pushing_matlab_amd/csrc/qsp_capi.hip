@@ -78,8 +78,8 @@ struct qsp_solver {
     int parts_req = 0;
     int fused_req = -1;            // QSP_FUSED_LOOP (-1: auto)
     bool nopack = false;           // QSP_PACKING=0: instances in lane order (developer A/B of the wave packing)
-    bool mfw = true;               // QSP_MFMA_WALK=0: the lane walk at 15 <= N <= 31 too (developer A/B; rounds
-                                   // differently, so the oracle twin does not follow it)
+    bool mfw = true;               // QSP_MFMA_WALK=0: the lane walk wherever the matrix cores would factorise
+                                   // (developer A/B; rounds differently: the oracle twin reads the same variable)
     int cus = 256;                 // compute units of the device (hipDeviceProp multiProcessorCount)
 };
 

@@ -413,7 +413,10 @@ __device__ __forceinline__ void dyn_step(const double a[6], const double B[8], c
 // and write the stage's K and [R~ | r~] back over its first 16 slots, which the stage lane collects
 // after the walk (forming -R~^-1 and kk itself, in parallel).  The records of a wave's G instances do not fit at once: the walk runs in two
 // phases (stages H .. N-1 with the terminal record, then 0 .. H-1).
-enum MfwSlot : int { R_A = 0, R_B = 6, R_BB = 14, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
+// (a record row-major in the order the block lanes read it: [B | b] row by row, so the lanes of two matrix
+// rows read at most six consecutive doubles per operand, which the three instances' records -- 9 apart
+// mod 32 at N = 20 -- keep on disjoint LDS banks)
+enum MfwSlot : int { R_G = 0, R_A = 12, R_GX = 18, R_HX3 = 22, R_HU = 23, R_GU = 25, MFW_REC = 27 };
 enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 of Z = [R~ | r~ | .]
 // the operand constants (A's ones and zeros, the zero column of [B | b | 0], Hx's fixed diagonal), at the
 // end of the region: the lanes whose operand element is one read it there instead of from the record
@@ -473,7 +476,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     int ao = -1;
     if (cc >= 2 && r < 2) ao = R_A + 2 * r + (cc - 2);
     else if (cc == 3 && r >= 2) ao = R_A + 2 + r;
-    const int go = cc < 2 ? R_B + 2 * r + cc : (cc == 2 ? R_BB + r : -1);
+    const int go = cc < 3 ? R_G + 3 * r + cc : -1;
     const int ho = (r == 3 && cc == 3) ? R_HX3 : -1;   // Q's C (Hx): only hx3 varies
     int zo = -1;                                       // Z's C: Hu on the diagonal, gu in column 2
     if (r < 2 && r == cc) zo = R_HU + r;
@@ -495,9 +498,11 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
 #pragma unroll
                     for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[0][q];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[0][q];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[0][q];
+                    for (int q = 0; q < 4; ++q) {
+                        rw[R_G + 3 * q] = st.B[0][2 * q];
+                        rw[R_G + 3 * q + 1] = st.B[0][2 * q + 1];
+                        rw[R_G + 3 * q + 2] = st.bb[0][q];
+                    }
 #pragma unroll
                     for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[0][q];
                     rw[R_GX + 3] = gx3[0];
@@ -521,9 +526,11 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     #pragma unroll
                         for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[ls][q];
     #pragma unroll
-                        for (int q = 0; q < 8; ++q) rw[R_B + q] = st.B[ls][q];
-    #pragma unroll
-                        for (int q = 0; q < 4; ++q) rw[R_BB + q] = st.bb[ls][q];
+                        for (int q = 0; q < 4; ++q) {
+                            rw[R_G + 3 * q] = st.B[ls][2 * q];
+                            rw[R_G + 3 * q + 1] = st.B[ls][2 * q + 1];
+                            rw[R_G + 3 * q + 2] = st.bb[ls][q];
+                        }
     #pragma unroll
                         for (int q = 0; q < 3; ++q) rw[R_GX + q] = st.g[ls][q];
                         rw[R_GX + 3] = gx3[ls];
@@ -618,7 +625,8 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
 #pragma unroll
                 for (int q = 0; q < 8; ++q) st.K[0][q] = rr[O_K + q];
                 // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
-                const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
+                const double* rz = rr + O_Z;
+                const double R00 = rz[0], R01 = rz[1], rt0 = rz[2], R11 = rz[5], rt1 = rz[6];
                 const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
                 st.Rn[0][0] = (-R11) * idet;
                 st.Rn[0][1] = R01 * idet;
@@ -635,7 +643,8 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     #pragma unroll
                     for (int q = 0; q < 8; ++q) st.K[ls][q] = rr[O_K + q];
                     // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
-                    const double R00 = rr[O_Z], R01 = rr[O_Z + 1], rt0 = rr[O_Z + 2], R11 = rr[O_Z + 5], rt1 = rr[O_Z + 6];
+                    const double* rz = rr + O_Z;
+                    const double R00 = rz[0], R01 = rz[1], rt0 = rz[2], R11 = rz[5], rt1 = rz[6];
                     const double idet = rcp(qfma(R00, R11, -(R01 * R01)));
                     st.Rn[ls][0] = (-R11) * idet;
                     st.Rn[ls][1] = R01 * idet;
