@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 OUT=${OUT:-gpurun_out/pmc}
-ARGS=${ARGS:-"--no-cpu --no-configs1 --no-configs4 --no-closed-loop --steps 1 --warmup 0"}
+ARGS=${ARGS:-"--no-cpu --no-configs1 --no-configs4 --no-closed-loop --no-qp50 --steps 1 --warmup 0"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
