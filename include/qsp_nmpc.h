@@ -102,7 +102,7 @@ typedef struct {
     int32_t factor_scan;      /* two stages per lane (S = 2: N + 1 > 32, e.g. N = 50) only.  0 (default): the
                                  Riccati factorisation walks the horizon stage by stage, as at S = 1 and in
                                  HPIPM.  1: it runs as an associative (parallel-in-time) scan of the stages'
-                                 value-function elements -- configs[4] 94k -> 115k solves/s on one MI355X, but
+                                 value-function elements -- configs[4] 110k -> 115k solves/s on one MI355X, but
                                  about two digits less accurate (u0 vs the extended-precision oracle: median
                                  8e-11 instead of 2e-12 after 5 SQP iterations), which the fixed-K SQP's
                                  rounding sensitivity turns into more lanes off the reference */
@@ -153,9 +153,10 @@ int qsp_get_layout(const qsp_solver* s, int32_t* stages_per_lane, int32_t* lanes
  * ocp_opts, NMPC_controller.m:270-300).  The choice follows N, the layout and factor_scan, and it fixes
  * the rounding order of every result: */
 #define QSP_WALK_LANE 0   /* the Riccati recursion as 4x4 algebra on one lane per stage, handed lane to lane */
-#define QSP_WALK_MFMA 1   /* on the FP64 matrix cores (v_mfma_f64_4x4x4_4b_f64, one instance per 16-lane
-                             block): the factorisation, and at one stage per lane (15 <= N <= 31) the
-                             closed-loop forward and difference walks too; two stages per lane: every N */
+#define QSP_WALK_MFMA 1   /* the factorisation on the FP64 matrix cores (v_mfma_f64_4x4x4_4b_f64, one
+                             instance per 16-lane block): at one stage per lane for 15 <= N <= 31, at two
+                             stages per lane for every N.  The closed-loop forward and difference passes
+                             stay lane walks (at two stages per lane: scans) */
 #define QSP_WALK_SCAN 2   /* factor_scan = 1 at two stages per lane: the associative scan */
 int qsp_get_factor_walk(const qsp_solver* s, int32_t* walk);
 
