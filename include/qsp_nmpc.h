@@ -154,8 +154,8 @@ int qsp_get_layout(const qsp_solver* s, int32_t* stages_per_lane, int32_t* lanes
  * the rounding order of every result: */
 #define QSP_WALK_LANE 0   /* the Riccati recursion as 4x4 algebra on one lane per stage, handed lane to lane */
 #define QSP_WALK_MFMA 1   /* the factorisation on the FP64 matrix cores (v_mfma_f64_4x4x4_4b_f64, one
-                             instance per 16-lane block): at one stage per lane for 15 <= N <= 31, at two
-                             stages per lane for every N.  The closed-loop forward and difference passes
+                             instance per 16-lane block): at one stage per lane for 12 <= N <= 31, at two
+                             stages per lane from N = 24 (four instances per wave or fewer).  The closed-loop forward and difference passes
                              stay lane walks (at two stages per lane: scans) */
 #define QSP_WALK_SCAN 2   /* factor_scan = 1 at two stages per lane: the associative scan */
 int qsp_get_factor_walk(const qsp_solver* s, int32_t* walk);
@@ -293,8 +293,8 @@ int qsp_synchronize(qsp_solver* s);
  * counterpart (an execution choice of the batched engine).  get: the count the next solve uses.
  * Batches whose waves fit the GPU's SIMDs once (nlp_mode 0) run the whole SQP loop in one launch
  * instead (one part; environment QSP_FUSED_LOOP=0/1 at qsp_create overrides the automatic choice).
- * The Riccati factorisation runs on the FP64 matrix cores at one stage per lane for 15 <= N <= 31 and at
- * two stages per lane for every N (qsp_get_factor_walk reports it); environment
+ * The Riccati factorisation runs on the FP64 matrix cores at one stage per lane for 12 <= N <= 31 and at
+ * two stages per lane from N = 24 (qsp_get_factor_walk reports it); environment
  * QSP_MFMA_WALK=0 at qsp_create selects the lane walk instead, a developer A/B that rounds differently
  * (the oracle twin follows the same variable). */
 int qsp_set_stream_parts(qsp_solver* s, int32_t parts);

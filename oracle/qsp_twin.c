@@ -383,14 +383,14 @@ static void make_par(tw_par *p, const or_opts *o)
     p->s0_bound = o->stage0_s_bound ? 1 : 0;
     p->factor_scan = o->factor_scan ? 1 : 0;
     /* the kernels factorise on the matrix cores where one instance per 16-lane block and a phase's
-     * stage records fit (mfw_fits: one stage per lane at 15 <= N <= 31, two stages per lane from four
+     * stage records fit (mfw_fits: one stage per lane at 12 <= N <= 31, two stages per lane from four
      * instances per wave down), unless the library's developer switch QSP_MFMA_WALK=0 selects the lane
      * walk there too */
     const char *mw = getenv("QSP_MFMA_WALK");
     {
         const int G = 64 / p->L, H = (p->N + 1) / 2, CM = p->N + 1 - H;
         const int cap = (p->S == 1 ? 12 + 2 : 24 + 4) * 64;   /* F_VA .. F_HG per slot + mfw_extra, x 64 lanes */
-        const int fits = G <= 4 && G * CM * 27 + 5 <= cap && (p->S == 2 || (p->N >= 15 && p->N <= 31));   /* + 5 constants */
+        const int fits = G <= 4 && G * CM * 27 + 5 <= cap && (p->S == 2 || p->N <= 31);   /* + 5 constants */
         p->mfma_walk = fits && !(mw && mw[0] == '0') && !o->lane_walk;
     }
     p->Ts = o->Ts;

@@ -9,6 +9,8 @@
 //   3  one product chained through its B operand (x = mfma(c, x, 0))
 //   4  one product chained through its C operand (x = mfma(a, b, x))
 //   5  the R~ gather and inverse alone (permlane16_swap, DPP broadcasts, det, rcp: VALU chain)
+//   6  four independent product chains (x_i = mfma(a, b, x_i)): the matrix-core pipe's issue rate
+//   7  eight independent product chains
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -33,7 +35,7 @@ __global__ void __launch_bounds__(64) steps(const double* in, double* out, long 
     const int r = l >> 4, cc = l & 3;
     double P = in[l], pv = cc == 2 ? in[64 + l] : 0.0;
     const double Am = in[128 + l], G2 = in[192 + l], CH = in[256 + l], CZ = in[320 + l], gq = cc == 2 ? in[384 + l] : 0.0;
-    double acc = 0.0;
+    double acc = 0.0, gqv = gq, e0 = 0.1, e1 = 0.2, e2 = 0.3, e3 = 0.4;
     __syncthreads();
     const long long t0 = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < n; ++k) {
@@ -76,6 +78,20 @@ __global__ void __launch_bounds__(64) steps(const double* in, double* out, long 
             P = mfma4(G2, P, 0.0);
         } else if constexpr (V == 4) {
             P = mfma4(G2, Am, P);
+        } else if constexpr (V == 6) {
+            P = mfma4(G2, Am, P);
+            pv = mfma4(G2, Am, pv);
+            acc = mfma4(CH, Am, acc);
+            gqv = mfma4(CZ, Am, gqv);
+        } else if constexpr (V == 7) {
+            P = mfma4(G2, Am, P);
+            pv = mfma4(G2, Am, pv);
+            acc = mfma4(CH, Am, acc);
+            gqv = mfma4(CZ, Am, gqv);
+            e0 = mfma4(G2, CH, e0);
+            e1 = mfma4(G2, CZ, e1);
+            e2 = mfma4(CH, CZ, e2);
+            e3 = mfma4(CZ, CH, e3);
         } else {
             const auto slo = __builtin_amdgcn_permlane16_swap(__double2loint(P), __double2loint(P), false, false);
             const auto shi = __builtin_amdgcn_permlane16_swap(__double2hiint(P), __double2hiint(P), false, false);
@@ -86,7 +102,7 @@ __global__ void __launch_bounds__(64) steps(const double* in, double* out, long 
         }
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
-    out[blockIdx.x * 64 + l] = P + pv + acc;
+    out[blockIdx.x * 64 + l] = P + pv + acc + gqv + e0 + e1 + e2 + e3;
     if (l == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
@@ -122,6 +138,8 @@ int main() {
         run<3>("one product chained through B", din, dout, dcyc, blocks);
         run<4>("one product chained through C", din, dout, dcyc, blocks);
         run<5>("R~ gather + 2x2 inverse alone", din, dout, dcyc, blocks);
+        run<6>("4 independent product chains (4 products)", din, dout, dcyc, blocks);
+        run<7>("8 independent product chains (8 products)", din, dout, dcyc, blocks);
     }
     return 0;
 }

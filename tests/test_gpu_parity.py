@@ -282,7 +282,9 @@ def test_horizon_and_layout_edges(oracle, N, S):
 
 
 @pytest.mark.parametrize("N, kw, want", [
-    (14, {}, "lane walk"),                                        # five instances per wave: no block each
+    (11, {}, "lane walk"),                                        # five instances per wave: no block each
+    (12, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),          # four instances per wave
+    (14, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),
     (15, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),
     (20, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),          # the headline
     (31, {}, "matrix cores (v_mfma_f64_4x4x4_4b_f64)"),

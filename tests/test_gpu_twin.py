@@ -280,13 +280,13 @@ def test_qp_divergence_exit_bit_identical(twin, mu_max):
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])
-@pytest.mark.parametrize("N,S", [(1, 1), (2, 1), (2, 2), (14, 1), (15, 1), (21, 1), (31, 1), (32, 0), (32, 1), (63, 1),
+@pytest.mark.parametrize("N,S", [(1, 1), (2, 1), (2, 2), (11, 1), (12, 1), (14, 1), (15, 1), (21, 1), (31, 1), (32, 0), (32, 1), (63, 1),
                                  (63, 2), (100, 2), (127, 2)])
 def test_horizons_and_layouts_bit_identical(twin, monkeypatch, N, S, fused):
     """Every lane layout the library accepts, at its edges: one stage per lane from N = 1 (32 instances
     per wave) to N = 63 (one instance filling the wave), two stages per lane up to N = 127; the auto
-    choice at N = 32 (two stages per lane); the matrix-core factorisation's range 15 <= N <= 31 (four
-    instances per wave at N = 15, two from N = 21) and the lane walk just below it (N = 14); 97 lanes
+    choice at N = 32 (two stages per lane); the matrix-core factorisation's range 12 <= N <= 31 (four
+    instances per wave at N = 12 ... 15, two from N = 21) and the lane walk just below it (N = 11); 97 lanes
     (a partly filled last wave), mixed shapes, both the per-iteration launches and the fused
     small-batch loop (QSP_FUSED_LOOP)."""
     from bench import SEED, make_inputs

@@ -174,7 +174,7 @@ def test_layouts_differ_by_rounding_only(twin):
 
 
 def test_mfma_walk_matches_lane_walk(twin, monkeypatch):
-    """The matrix-core factorisation (the default at one stage per lane, 15 <= N <= 31) against the lane
+    """The matrix-core factorisation (the default at one stage per lane, 12 <= N <= 31) against the lane
     walk (QSP_MFMA_WALK=0), both measured against the literal formulas in __float128: three SQP-RTI
     iterations of 64 lanes, mixed shapes, at the range's lower edge and the bench horizon.  The two walks
     associate every product differently (their answers part after the first iteration) and are equally

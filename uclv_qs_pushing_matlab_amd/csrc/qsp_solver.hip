@@ -421,7 +421,7 @@ enum MfwOut : int { O_K = 0, O_Z = 8, O_COUNT = 16 };   // K (2 x 4), rows 0, 1 
 // the operand constants (A's ones and zeros, the zero column of [B | b | 0], Hx's fixed diagonal), at the
 // end of the region: the lanes whose operand element is one read it there instead of from the record
 enum MfwConst : int { C_ONE = 0, C_ZERO = 1, C_HX = 2, C_COUNT = 5 };
-static_assert((F_COUNT - F_VA + mfw_extra<1>()) * BLOCK >= 33 * MFW_REC + C_COUNT, "S = 1: records of G (N/2 + 1) stages, 15 <= N <= 31");
+static_assert((F_COUNT - F_VA + mfw_extra<1>()) * BLOCK >= 33 * MFW_REC + C_COUNT, "S = 1: records of G (N/2 + 1) stages, 12 <= N <= 31");
 static_assert(((F_COUNT - F_VA) * 2 + mfw_extra<2>()) * BLOCK >= 64 * MFW_REC + C_COUNT, "S = 2: records of G (N/2 + 1) stages, N <= 127");
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {   // a'b + c per 4x4 block
@@ -446,13 +446,13 @@ __device__ __forceinline__ double quad_bcast(double v) {   // DPP quad_perm: one
 template <int S>
 constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + mfw_extra<S>()) * BLOCK; }
 // Which horizons factorise on the matrix cores: one instance per 16-lane block (G <= 4: at one
-// stage per lane N >= 15, at two always), the records of a phase in the region.  One stage per lane
+// stage per lane N >= 12, at two N >= 24), the records of a phase in the region.  One stage per lane
 // takes the walk as its ALT kernel variant; two stages per lane by a uniform switch, since
 // ALT is the factorisation scan there.
 __host__ __device__ __forceinline__ bool mfw_fits(int N, int S) {
     const int L = (N + S) / S, G = 64 / L, H = (N + 1) / 2, CM = N + 1 - H;
     const int cap = S == 1 ? mfw_region<1>() : mfw_region<2>();
-    return G <= 4 && G * CM * MFW_REC + C_COUNT <= cap && (S == 2 || (N >= 15 && N <= 31));
+    return G <= 4 && G * CM * MFW_REC + C_COUNT <= cap && (S == 2 || N <= 31);
 }
 __host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p, int S) {
     return p.mfma_walk != 0 && mfw_fits(p.N, S);

@@ -47,7 +47,7 @@ struct SolveParams {
     int32_t s0_bound;                             // 1: the s bound of h also applies at stage 0
     int32_t factor_scan;                          // 1: S = 2 factorisation as an associative scan (qsp_options)
     int32_t mfma_walk;                            // 1: factorisation on the FP64 matrix cores where it fits (mfw_fits:
-                                                  // S = 1 at 15 <= N <= 31, S = 2 at every N)
+                                                  // S = 1 at 12 <= N <= 31, S = 2 from N = 24)
     double tol_stat, tol_eq, tol_ineq, tol_comp;  // nlp_mode 1 termination
     double ls_alpha_min, ls_alpha_red, ls_eps;    // nlp_mode 1 line search
     CtrlParams cp;
