@@ -17,7 +17,7 @@ NAMES = {0: "iteration head (mu, stop tests, ballot)", 1: "barrier_terms", 2: "f
          3: "predictor forward walk", 4: "affine directions, step, mu_aff", 5: "corrector_terms",
          6: "corrector difference walk", 7: "corrector forward walk", 8: "corrector directions, step, update",
          10: "kernel head: linearisation, loads", 11: "qp_ipm total", 12: "rollout, adjoint, stores",
-         13: "qp_ipm start point"}
+         13: "qp_ipm start point", 14: "head: permutation and iterate loads", 15: "head: RK4 + sensitivities"}
 
 
 def main():
@@ -57,7 +57,7 @@ def main():
     assert L.qsp_debug_segments(seg.ctypes.data, 1) == 0
     seg = seg.astype(np.float64)
     iters = seg[31]
-    kern = seg[10] + seg[11] + seg[12]
+    kern = seg[10] + seg[11] + seg[12] + seg[14] + seg[15]
     out = {"workload": f"N={args.N} batch={args.batch}", "wall_s": wall, "wave_ipm_iterations": iters,
            "kernel_wave_cycles": kern, "segments": {}}
     print(f"solve wall {wall * 1e3:.1f} ms; wave IPM iterations {iters:.0f}; kernel wave cycles {kern:.3e} "

@@ -1860,8 +1860,22 @@ __global__ void __launch_bounds__(BLOCK, QSP_MIN_WAVES) qp_step_kernel(SolveArgs
             if (kc < N && lin_live) {
                 const double xk[4] = {X[4 * kc], X[4 * kc + 1], X[4 * kc + 2], X[4 * kc + 3]};
                 const double uk[2] = {U[2 * kc], U[2 * kc + 1]};
+#ifdef QSP_SEGSTAMP
+                {   // (diagnostic build: the iterate's loads complete before the stamp)
+                    double w = xk[0] + xk[1] + xk[2] + xk[3] + uk[0] + uk[1];
+                    asm volatile("" : "+v"(w));
+                    SEG_NEXT(14, t_k);
+                }
+#endif
                 Lin Ln;
                 rk4<true>(shape_of(A, iv), p.Ts, xk, uk, Ln);
+#ifdef QSP_SEGSTAMP
+                {
+                    double w = Ln.a[0] + Ln.B[0] + Ln.xn[0];
+                    asm volatile("" : "+v"(w));
+                    SEG_NEXT(15, t_k);
+                }
+#endif
                 const double* yr = A.yref + ((size_t)iv * N + kc) * 6;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) st.a[ls][q] = Ln.a[q];
