@@ -658,8 +658,8 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
     }
     // the overlaid fields read later: the terminal and padding slots' F_VA / F_VN stay zero (the
     // forward passes write them on the stages k < N only; qp_ipm's start defines them)
-    // (one stage per lane: written as the lane test, which keeps the kernel at 247 registers; the
-    // unrolled slot loop, the same test, costs it the second wave per SIMD)
+    // (one stage per lane: written as the lane test, which keeps the kernel within two waves per SIMD
+    // (249 registers); the unrolled slot loop, the same test, costs it the second wave)
     if constexpr (S == 1) {
         if (c.lig >= N) {
 #pragma unroll
