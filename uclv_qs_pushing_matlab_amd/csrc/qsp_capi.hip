@@ -135,6 +135,7 @@ static void fill_params(qsp_solver* s) {
     p.s0_bound = s->o.stage0_s_bound ? 1 : 0;
     p.factor_scan = s->o.factor_scan ? 1 : 0;
     p.mfma_walk = s->mfw ? 1 : 0;
+    mfw_prepare(p);
     p.qp_stall_iters = s->o.qp_stall_iters;
     p.qp_stall_alpha = s->o.qp_stall_alpha;
     p.qp_mu_max = s->o.qp_mu_max;
@@ -445,6 +446,7 @@ int qsp_create(const qsp_options* o, qsp_solver** out) {
     if (const char* pk = std::getenv("QSP_PACKING")) s->nopack = pk[0] == '0';
     if (const char* mw = std::getenv("QSP_MFMA_WALK")) s->mfw = mw[0] != '0';
     s->p.mfma_walk = s->mfw ? 1 : 0;
+    mfw_prepare(s->p);
     const char* pz = std::getenv("QSP_DEBUG_POISON");
     s->poison = pz && pz[0] == '1';
     if (s->poison) {

@@ -66,6 +66,7 @@ struct SolveArgs {
 int lanes_per_instance(int N, int S);
 // QSP_WALK_* of a handle's QP kernels (the same rule the launchers apply: mfw_use, factor_scan)
 int factor_walk_kind(const SolveParams& p, int S);
+void mfw_prepare(SolveParams& p);   // SolveParams::mfw_on / mfw_is from N and mfma_walk
 // Multi-stream split of the SQP loop (SqpStreams::parts = P > 1): the instances are cut into
 // P parts and each part runs its own (sort, qp_step) sequence on its own stream (part 0 on
 // the solve's stream, part p on aux[p-1]), so the launch tail of one part's QP overlaps the

@@ -449,13 +449,31 @@ constexpr int mfw_region() { return ((F_COUNT - F_VA) * S + mfw_extra<S>()) * BL
 // stage per lane N >= 12, at two N >= 24), the records of a phase in the region.  One stage per lane
 // takes the walk as its ALT kernel variant; two stages per lane by a uniform switch, since
 // ALT is the factorisation scan there.
+// The instances' record regions start IS doubles apart, IS >= CM records: a stride whose multiples put
+// the instances' reads of one operand (at most six consecutive doubles per half wave) on disjoint LDS banks
+// (32 doubles): 9 ... 11 or 21 ... 23 mod 32 for three instances, 8 or 24 for four, 6 ... 26 for two.
+__host__ __device__ __forceinline__ int mfw_stride(int CM, int G) {
+    const int rs = CM * MFW_REC;
+    for (int is = rs;; ++is) {
+        const int m = is & 31;
+        if (G <= 1 || (G == 2 && m >= 6 && m <= 26) || (G == 3 && ((m >= 9 && m <= 11) || (m >= 21 && m <= 23))) ||
+            (G >= 4 && (m == 8 || m == 24)))
+            return is;
+    }
+}
 __host__ __device__ __forceinline__ bool mfw_fits(int N, int S) {
     const int L = (N + S) / S, G = 64 / L, H = (N + 1) / 2, CM = N + 1 - H;
     const int cap = S == 1 ? mfw_region<1>() : mfw_region<2>();
-    return G <= 4 && G * CM * MFW_REC + C_COUNT <= cap && (S == 2 || N <= 31);
+    return G <= 4 && (G - 1) * mfw_stride(CM, G) + CM * MFW_REC + C_COUNT <= cap && (S == 2 || N <= 31);
 }
-__host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p, int S) {
-    return p.mfma_walk != 0 && mfw_fits(p.N, S);
+__host__ __device__ __forceinline__ bool mfw_use(const SolveParams& p, int S) { return p.mfw_on[S - 1] != 0; }
+// (host, whenever N or mfma_walk change: the kernels read the choice and the stride instead of searching it)
+void mfw_prepare(SolveParams& p) {
+    for (int S = 1; S <= 2; ++S) {
+        const int L = (p.N + S) / S, G = 64 / L, H = (p.N + 1) / 2, CM = p.N + 1 - H;
+        p.mfw_on[S - 1] = p.mfma_walk != 0 && mfw_fits(p.N, S);
+        p.mfw_is[S - 1] = G >= 1 && G <= 4 ? mfw_stride(CM, G) : CM * MFW_REC;
+    }
 }
 
 template <int S>
@@ -463,6 +481,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
                                                  const double (&hu)[S][2], const double (&gx3)[S], const double (&gu)[S][2]) {
     const int N = c.N, G = 64 / c.L;
     const int H = (N + 1) / 2, CM = N + 1 - H;   // phase split; records per instance and phase
+    const int IS = p.mfw_is[S - 1];               // doubles from one instance's records to the next's (mfw_prepare)
     double* const reg = st.lds - (threadIdx.x & 63) + F_VA * S * BLOCK;
     // block-lane geometry and the record slot of each operand element (-1: structural constant)
     // (an opaque lane id: derived from c.lane, the geometry would be hoisted out of the IPM loop and
@@ -493,7 +512,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
         // as the lane test: the slot loop, the same test, costs the S = 1 kernel 2 % in issue order)
         if constexpr (S == 1) {
             if (c.grp < G && c.lig >= kb && c.lig <= ke) {
-                double* rw = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+                double* rw = reg + c.grp * IS + (c.lig - kb) * MFW_REC;
                 if (c.lig < N) {
 #pragma unroll
                     for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[0][q];
@@ -521,7 +540,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             for (int ls = 0; ls < S; ++ls) {
                 const int k = kof<S>(c, ls);
                 if (c.grp < G && k >= kb && k <= ke) {
-                    double* rw = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+                    double* rw = reg + c.grp * IS + (k - kb) * MFW_REC;
                     if (k < N) {
     #pragma unroll
                         for (int q = 0; q < 6; ++q) rw[R_A + q] = st.a[ls][q];
@@ -547,7 +566,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             }
         }
         wave_lds_sync();
-        const double* rb = reg + bg * CM * MFW_REC;   // this block's records of the phase
+        const double* rb = reg + bg * IS;   // this block's records of the phase
         if (ph == 0) {
             P = r == cc ? (r == 0 ? p.We[0] : (r == 1 ? p.We[1] : (r == 2 ? p.We[2] : p.We[3]))) : 0.0;
             pv = cc == 2 ? rb[(N - kb) * MFW_REC + R_GX + r] : 0.0;   // p_N = g_N (column 2)
@@ -556,7 +575,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
         // one step of the walk from its operand elements (Am: A, G2: [B | b | 0], CH and CZ: the C operands
         // of Q and Z, gq: gx); p lives in column 2 of pv, zero in the others, so T2 takes it as its C operand
         auto step = [&](int k, double Am, double G2, double CH, double CZ, double gq) {
-            double* rk = reg + (bg * CM + (k - kb)) * MFW_REC;
+            double* rk = reg + bg * IS + (k - kb) * MFW_REC;
             const double T1 = mfma4(P, Am, 0.0);                    // P'A
             const double T2 = mfma4(P, G2, pv);                     // P'[B | b | 0] + [0 | 0 | p | 0]
             const double Y = mfma4(G2, T1, 0.0);                    // rows 0, 1: S~ = B'P'A
@@ -621,7 +640,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
         // collect: the stage lanes take their slots' factors (stages k < N)
         if constexpr (S == 1) {
             if (c.grp < G && c.lig >= kb && c.lig <= ke && c.lig < N) {
-                const double* rr = reg + (c.grp * CM + (c.lig - kb)) * MFW_REC;
+                const double* rr = reg + c.grp * IS + (c.lig - kb) * MFW_REC;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) st.K[0][q] = rr[O_K + q];
                 // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)
@@ -639,7 +658,7 @@ __device__ __forceinline__ void factor_walk_mfma(const Ctx& c, const SolveParams
             for (int ls = 0; ls < S; ++ls) {
                 const int k = kof<S>(c, ls);
                 if (c.grp < G && k >= kb && k <= ke && k < N) {
-                    const double* rr = reg + (c.grp * CM + (k - kb)) * MFW_REC;
+                    const double* rr = reg + c.grp * IS + (k - kb) * MFW_REC;
     #pragma unroll
                     for (int q = 0; q < 8; ++q) st.K[ls][q] = rr[O_K + q];
                     // Rn = -R~^-1 and kk = -R~^-1 r~ from the R~ the walk inverted (the same operations)

@@ -48,6 +48,9 @@ struct SolveParams {
     int32_t factor_scan;                          // 1: S = 2 factorisation as an associative scan (qsp_options)
     int32_t mfma_walk;                            // 1: factorisation on the FP64 matrix cores where it fits (mfw_fits:
                                                   // S = 1 at 12 <= N <= 31, S = 2 from N = 24)
+    int32_t mfw_on[2];                            // per stages-per-lane S = 1, 2: mfma_walk and the records fit
+    int32_t mfw_is[2];                            // ... and the doubles between instances' record regions
+                                                  // (mfw_prepare, host-side: the kernels only read them)
     double tol_stat, tol_eq, tol_ineq, tol_comp;  // nlp_mode 1 termination
     double ls_alpha_min, ls_alpha_red, ls_eps;    // nlp_mode 1 line search
     CtrlParams cp;
